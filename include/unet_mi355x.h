@@ -1,0 +1,132 @@
+/* unet_mi355x.h -- C-ABI of the MI355X-native UNet forward path.
+ *
+ * Drop-in for the reference segmentation call surface (tingyu-c/TW-invoice-unet-ocr-llm):
+ *   unet_model.UNet(n_channels, n_classes)      unet_model.py:23-53   -> unet_create
+ *   model.load_state_dict(torch.load(ckpt))     inference.py:17-24     -> unet_load_weights
+ *   model(x)  (UNet.forward)                    unet_model.py:55-86    -> unet_forward (logits)
+ *   sigmoid + per-field thresholds              inference.py:72-79     -> unet_forward (masks)
+ *
+ * The reference has no FFI (it is pure Python on torch); this header is the boundary a
+ * ctypes/cffi binding loads.  Plain C types only; no torch or C++ types cross it.
+ *
+ * Conventions
+ *   - return value: 0 = OK, negative = error (UNET_E*); unet_last_error() gives the
+ *     message for the calling thread.  C++ exceptions never cross the ABI.
+ *   - device pointers are caller-owned (e.g. torch data_ptr()); work is enqueued on the
+ *     caller's HIP stream (hipStream_t passed as void*), with no hidden synchronisation
+ *     except inside unet_load_weights / unet_reserve (allocation + upload).
+ *   - a handle is not re-entrant: it owns one workspace.  Use one handle per device and
+ *     serialise calls on it (the Python wrapper does).
+ */
+#ifndef UNET_MI355X_H
+#define UNET_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UNET_ABI_VERSION 1
+
+/* error codes */
+#define UNET_OK 0
+#define UNET_EINVAL (-1)     /* bad argument (maps to ValueError)                    */
+#define UNET_ESHAPE (-2)     /* unsupported shape, e.g. H or W not divisible by 16     */
+#define UNET_ENOMEM (-3)     /* device allocation failed                               */
+#define UNET_EHIP (-4)       /* HIP runtime error                                      */
+#define UNET_ESTATE (-5)     /* call out of order (e.g. forward before weights)       */
+#define UNET_EKEY (-6)       /* state_dict key missing / unexpected / wrong shape      */
+
+/* compute / storage dtype of the activations and packed weights (accumulation is fp32) */
+#define UNET_DTYPE_F32 0
+#define UNET_DTYPE_BF16 1
+#define UNET_DTYPE_F16 2
+
+/* input layouts / dtypes accepted by unet_forward */
+#define UNET_LAYOUT_NCHW 0
+#define UNET_IN_F32 0
+
+/* mask outputs of unet_forward */
+#define UNET_MASK_NONE 0
+#define UNET_MASK_U8 1    /* uint8 [N][n_classes][H][W], 1 where sigmoid(logit) > thr      */
+#define UNET_MASK_BITS 2  /* uint8 [N][n_classes][H][W/8], bit b of byte x/8 = pixel x      */
+
+typedef struct unet_handle unet_handle;
+
+typedef struct unet_config {
+  int n_channels;     /* input channels: 1 or 3 (UNet(n_channels=...), unet_model.py:24) */
+  int n_classes;      /* 1..4 (UNet(n_classes=...); the app uses 3)                       */
+  int dtype;          /* UNET_DTYPE_*                                                     */
+  int device;         /* HIP device ordinal                                               */
+  float thresholds[4];/* per-class probability thresholds (inference.py:76-78)           */
+} unet_config;
+
+typedef struct unet_tensor_view {
+  const char* name;   /* state_dict key, e.g. "down1.net.0.weight"                       */
+  const void* data;   /* host pointer, contiguous                                         */
+  int dtype;          /* 0 = float32, 1 = int64 (num_batches_tracked; ignored)            */
+  int ndim;
+  int64_t shape[4];
+} unet_tensor_view;
+
+/* Create a handle for UNet(n_channels, n_classes) on cfg->device.
+ * Replaces: unet_model.UNet.__init__ (unet_model.py:24-53). */
+int unet_create(const unet_config* cfg, unet_handle** out);
+
+/* Strictly load the 136-key reference state_dict (host fp32), fold eval BatchNorm
+ * (eps 1e-5) into the convs, pre-pack NHWC/MFMA panels and upload them.
+ * Replaces: load_state_dict(strict=True) + eval() (inference.py:20-23). */
+int unet_load_weights(unet_handle* h, const unet_tensor_view* tensors, int n);
+
+/* Bytes of device workspace unet_forward needs for (N, H, W). */
+size_t unet_workspace_bytes(const unet_handle* h, int N, int H, int W);
+
+/* Allocate (grow) the workspace for up to (N, H, W) so that later unet_forward calls
+ * neither allocate nor synchronise (graph-capturable). */
+int unet_reserve(unet_handle* h, int N, int H, int W);
+
+/* Forward pass.  x: device fp32 NCHW [N][n_channels][H][W].
+ * logits: device fp32 NCHW [N][n_classes][H][W] or NULL.
+ * masks:  device uint8 per mask_kind or NULL (mask_kind UNET_MASK_NONE).
+ * H, W must be divisible by 16 (the reference raises inside torch.cat otherwise).
+ * Replaces: UNet.forward (unet_model.py:55-86) and inference.py:72-79. */
+int unet_forward(unet_handle* h, const void* x, int x_layout, int x_dtype,
+                 void* logits, void* masks, int mask_kind,
+                 int N, int H, int W, void* hip_stream);
+
+/* Number of kernel launches in one forward (first conv, 17 implicit-GEMM 3x3 convs with
+ * the fused pool / head epilogues, 4 ConvTranspose2d), in execution order:
+ * down1.0 down1.3 down2.0 down2.3 down3.0 down3.3 down4.0 down4.3 bottleneck.0
+ * bottleneck.3 up4 conv4.0 conv4.3 up3 conv3.0 conv3.3 up2 conv2.0 conv2.3 up1 conv1.0
+ * conv1.3+out_conv. */
+#define UNET_NUM_LAUNCHES 22
+int unet_num_launches(void);
+
+/* unet_forward, plus HIP-event timing of every launch on the given stream (ms, in the
+ * order above, launch_ms[UNET_NUM_LAUNCHES]).  Synchronises on the stream; for
+ * measurement only. */
+int unet_forward_timed(unet_handle* h, const void* x, int x_layout, int x_dtype,
+                       void* logits, void* masks, int mask_kind,
+                       int N, int H, int W, void* hip_stream, float* launch_ms);
+
+/* Copy an intermediate activation of the last forward (debug / per-layer parity):
+ * name in {"c1","p1","c2","p2","c3","p3","c4","p4","bn","c7","u1","u2","u3","u4","c8a"}
+ * (c_k: encoder skips, p_k: pooled maps, u_k: ConvTranspose outputs, c7: conv2 output,
+ * c8a: conv1.net.0 output).
+ * dst: device buffer receiving fp32 NCHW [N][C][h][w]; *numel receives the element count
+ * when dst is NULL. */
+int unet_debug_fetch(unet_handle* h, const char* name, float* dst, size_t* numel, void* hip_stream);
+
+int unet_destroy(unet_handle* h);
+
+/* Message of the last error on this thread ("" if none). */
+const char* unet_last_error(void);
+
+int unet_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UNET_MI355X_H */

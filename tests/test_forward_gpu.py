@@ -1,0 +1,170 @@
+"""Parity of the native MI355X forward (through the C-ABI) against the golden vectors the
+reference produced and against the CPU oracle.  Needs a GPU: run with -m gpu.
+
+Tolerances (max |err| / max(1, max|ref|)):
+  fp32 path (exact-fp32 MFMA, different summation order)  <= 1e-4
+  fp16 path (fp16 storage, fp32 accumulate)                <= 1.5e-2
+  bf16 path (bf16 storage, fp32 accumulate)                <= 8e-2
+Masks (fp32 path) must match the oracle to IoU >= 0.999 (north_star); 16-bit IoUs are
+reported and bounded below.
+"""
+import glob
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import unet_oracle as orc
+from unet_mi355x import synthetic as syn
+from unet_mi355x.model import UNet
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOL = {"fp32": 1e-4, "fp16": 1.5e-2, "bf16": 8e-2}
+DEV = "cuda:0"
+
+
+def make_model(sd_np, c, dtype):
+    m = UNet(c, 3, compute_dtype=dtype)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd_np.items()})
+    return m.to(DEV).eval()
+
+
+def rel_err(out, ref):
+    return float(np.abs(out - ref).max()) / max(1.0, float(np.abs(ref).max()))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16"])
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "unet_*.npz"))), ids=os.path.basename)
+def test_golden_logits(path, dtype):
+    z = np.load(path)
+    c = int(z["n_channels"])
+    sd = syn.make_state_dict(int(z["seed"]), c, 3, profile=str(z["profile"]))
+    m = make_model(sd, c, dtype)
+    with torch.no_grad():
+        out = m(torch.from_numpy(z["x"]).to(DEV)).cpu().numpy()
+    err = rel_err(out, z["logits"])
+    print(f"{os.path.basename(path)} {dtype}: rel err {err:.3e}")
+    assert out.shape == z["logits"].shape
+    assert np.isfinite(out).all()
+    assert err <= TOL[dtype]
+    m.close()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_golden_intermediates(dtype):
+    """Per-layer localisation: skips, pools, bottleneck and up-convs vs the reference hooks."""
+    z = np.load(os.path.join(GOLD, "unet_c3_h16w16_n3_structured.npz"))
+    sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile=str(z["profile"]))
+    m = make_model(sd, 3, dtype)
+    x = torch.from_numpy(z["x"]).to(DEV)
+    with torch.no_grad():
+        m(x)
+    torch.cuda.synchronize()
+    for name, key in (("c1", "inter_c1"), ("c2", "inter_c2"), ("c3", "inter_c3"), ("c4", "inter_c4"),
+                      ("bn", "inter_bn"), ("u1", "inter_u1_up"), ("u4", "inter_u4_up"), ("c7", "inter_c7")):
+        ref = z[key]
+        got = m.intermediate(name).cpu().numpy().reshape(ref.shape)
+        err = rel_err(got, ref)
+        print(f"{name} {dtype}: rel err {err:.3e}")
+        assert err <= TOL[dtype], name
+    m.close()
+
+
+@pytest.mark.parametrize("c,n,h,w", [(3, 2, 64, 128), (1, 3, 96, 32), (3, 1, 160, 48)])
+def test_fp32_vs_oracle_odd_shapes(c, n, h, w):
+    sd = syn.make_state_dict(100 + h, c, 3, profile="structured")
+    x = syn.uniform_batch(5 + w, n, c, h, w)
+    ref = orc.unet_forward(sd, torch.from_numpy(x)).numpy()
+    m = make_model(sd, c, "fp32")
+    with torch.no_grad():
+        out = m(torch.from_numpy(x).to(DEV)).cpu().numpy()
+    err = rel_err(out, ref)
+    print(f"fp32 {c}x{h}x{w} n={n}: rel err {err:.3e}")
+    assert err <= TOL["fp32"]
+    m.close()
+
+
+def _recentred(seed, x, c=3):
+    """Structured weights with out_conv bias shifted so ~10% of pixels pass each threshold."""
+    sd = syn.make_state_dict(seed, c, 3, profile="structured")
+    logits = orc.unet_forward(sd, torch.from_numpy(x)).numpy()
+    thr = np.array([0.25, 0.40, 0.30])
+    q = np.quantile(logits.transpose(1, 0, 2, 3).reshape(3, -1), 0.9, axis=1)
+    sd["out_conv.bias"] = (sd["out_conv.bias"] + (np.log(thr / (1 - thr)) - q)).astype(np.float32)
+    return sd, orc.unet_forward(sd, torch.from_numpy(x)).numpy()
+
+
+def test_masks_512_all_dtypes():
+    """Full-size 512x512 pages: fused masks (u8 and bit-packed) vs the oracle's masks."""
+    x = syn.invoice_pages(21, 2, 512, 512, 3)
+    sd, ref_logits = _recentred(21, x)
+    ref_masks = np.stack([np.stack(list(orc.masks_from_logits(ref_logits[i]).values())) for i in range(2)])
+    xd = torch.from_numpy(x).to(DEV)
+    for dtype, min_iou in (("fp32", 0.999), ("fp16", 0.99), ("bf16", 0.95)):
+        m = make_model(sd, 3, dtype)
+        with torch.no_grad():
+            masks, logits = m.forward_masks(xd, with_logits=True)
+            bits = m.forward_masks(xd, packed=True)
+        masks = masks.cpu().numpy().astype(bool)
+        unpacked = np.unpackbits(bits.cpu().numpy(), axis=-1, bitorder="little").astype(bool)
+        assert np.array_equal(unpacked, masks), "bit-packed and u8 masks disagree"
+        ious = [orc.mask_iou(masks[i, k], ref_masks[i, k]) for i in range(2) for k in range(3)]
+        print(f"512x512 {dtype}: logits rel err {rel_err(logits.cpu().numpy(), ref_logits):.3e}, "
+              f"mask IoU min {min(ious):.5f} mean {np.mean(ious):.5f}")
+        assert min(ious) >= min_iou
+        m.close()
+
+
+def test_run_unet_boundary_matches_reference_golden():
+    """inference.run_unet (drop-in) on the golden 600x400 photo vs the reference's masks/crops."""
+    from PIL import Image
+    import hashlib
+    from unet_mi355x import inference as inf
+    z = np.load(os.path.join(GOLD, "run_unet_600x400.npz"))
+    sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile="structured")
+    sd["out_conv.bias"] = sd["out_conv.bias"] + z["out_bias_delta"]
+    assert syn.state_dict_checksum(sd) == str(z["sd_sha256"])
+    pil = Image.fromarray(z["image"], mode="RGB")
+    with tempfile.TemporaryDirectory() as td:
+        ck = os.path.join(td, "best_unet_model.pth")
+        torch.save({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, ck)
+        inf.DEVICE = DEV
+        masks, crops = inf.run_unet(pil, ck, compute_dtype="fp32")
+    for k in inf.FIELDS:
+        ref = np.unpackbits(z["maskbits_" + k], axis=-1, bitorder="little").astype(bool)
+        iou = orc.mask_iou(masks[k], ref)
+        print(f"run_unet {k}: IoU {iou:.6f}, differing pixels {int((masks[k] != ref).sum())}")
+        assert iou >= 0.999
+        if bool(z["crop_none_" + k]):
+            assert crops[k] is None
+        else:
+            arr = np.asarray(crops[k])
+            assert list(arr.shape) == list(z["crop_shape_" + k])
+            if np.array_equal(masks[k], ref):
+                assert hashlib.sha256(arr.tobytes()).hexdigest() == str(z["crop_sha256_" + k])
+
+
+def test_errors_and_no_fallback():
+    m = make_model(syn.make_state_dict(0, 3, 3), 3, "bf16")
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 3, 40, 32, device=DEV))
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 3, 32, 32))
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 1, 32, 32, device=DEV))
+    m.close()
+
+
+def test_weight_update_repacks():
+    sd = syn.make_state_dict(4, 3, 3)
+    m = make_model(sd, 3, "fp32")
+    x = torch.from_numpy(syn.uniform_batch(1, 1, 3, 32, 32)).to(DEV)
+    with torch.no_grad():
+        a = m(x).clone()
+        m.out_conv.bias.add_(1.0)
+        b = m(x)
+    assert torch.allclose(b - a, torch.ones_like(a), atol=1e-4)
+    m.close()

@@ -1,0 +1,71 @@
+"""The oracle (CPU restatement, oracle/unet_oracle.py) against the golden vectors the
+reference itself produced (tests/golden/make_golden.py).  CPU only."""
+import glob
+import hashlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import unet_oracle as orc
+from unet_mi355x import synthetic as syn
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+UNET_CASES = sorted(glob.glob(os.path.join(GOLD, "unet_*.npz")))
+
+
+def _sd_for(z):
+    c = int(z["n_channels"])
+    sd = syn.make_state_dict(int(z["seed"]), c, 3, profile=str(z["profile"]))
+    assert syn.state_dict_checksum(sd) == str(z["sd_sha256"]), "synthetic weight generator drifted"
+    return sd
+
+
+@pytest.mark.parametrize("path", UNET_CASES, ids=os.path.basename)
+def test_oracle_matches_reference_logits(path):
+    z = np.load(path)
+    sd = _sd_for(z)
+    out, inter = orc.unet_forward(sd, torch.from_numpy(z["x"]), return_intermediates=True)
+    ref = z["logits"]
+    scale = max(1.0, float(np.abs(ref).max()))
+    np.testing.assert_allclose(out.numpy(), ref, rtol=0, atol=2e-5 * scale)
+    for k in z.files:
+        if k.startswith("inter_") and k[6:] in inter:
+            r = z[k]
+            np.testing.assert_allclose(inter[k[6:]].numpy(), r, rtol=0, atol=2e-5 * max(1.0, float(np.abs(r).max())))
+
+
+def test_oracle_rejects_non_multiple_of_16():
+    sd = syn.make_state_dict(0, 3, 3)
+    with pytest.raises(RuntimeError):
+        orc.unet_forward(sd, torch.zeros(1, 3, 40, 32))
+
+
+def test_run_unet_postprocess_matches_reference():
+    """Oracle crop boxes + crops from the reference's own masks reproduce its crops."""
+    z = np.load(os.path.join(GOLD, "run_unet_600x400.npz"))
+    img = z["image"]
+    oh, ow = img.shape[:2]
+    masks = {k: np.unpackbits(z["maskbits_" + k], axis=-1, bitorder="little").astype(bool)
+             for k in orc.FIELDS}
+    boxes = orc.crop_boxes(masks, ow, oh)
+    for k in orc.FIELDS:
+        if bool(z["crop_none_" + k]):
+            assert boxes[k] is None or img[boxes[k][1]:boxes[k][3], boxes[k][0]:boxes[k][2]].mean() < 3
+            continue
+        x1, y1, x2, y2 = boxes[k]
+        crop = np.ascontiguousarray(img[y1:y2, x1:x2])
+        assert list(crop.shape) == list(z["crop_shape_" + k])
+        assert hashlib.sha256(crop.tobytes()).hexdigest() == str(z["crop_sha256_" + k])
+
+
+def test_mask_threshold_semantics():
+    """sigmoid + strict '>' in fp32 (inference.py:72-79)."""
+    thr_logit = np.log(0.25 / 0.75)
+    logits = np.zeros((3, 2, 2), np.float32)
+    logits[0, 0, 0] = thr_logit + 1e-3
+    logits[0, 0, 1] = thr_logit - 1e-3
+    m = orc.masks_from_logits(logits)
+    assert m["invoice_no"][0, 0] and not m["invoice_no"][0, 1]
+    assert orc.mask_iou(m["date"], m["date"]) == 1.0

@@ -1,0 +1,539 @@
+// C-ABI host layer of the MI355X UNet forward path (include/unet_mi355x.h).
+//
+// Owns: strict state_dict ingestion (unet_model.py:24-53 key set), eval-BatchNorm folding
+// (unet_model.py:11,15; eps 1e-5), weight pre-packing for the implicit-GEMM kernel, the
+// activation workspace, and the per-forward launch sequence that mirrors
+// UNet.forward (unet_model.py:55-86).
+#include "unet_internal.h"
+#include "../../include/unet_mi355x.h"
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+using namespace unet;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(UNET_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+uint16_t f32_to_bf16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+uint16_t f32_to_f16(float f) {
+  _Float16 h = (_Float16)f;
+  uint16_t r;
+  std::memcpy(&r, &h, 2);
+  return r;
+}
+
+// Packed-weight row permutation inside each 64-row group (see unet_kernels.hip
+// epilogue): packed row rho = t*16 + r holds natural row (r>>2)*16 + t*4 + (r&3).
+inline int natural_of_packed(int rho) {
+  const int g = rho & ~63, w = rho & 63, t = w >> 4, r = w & 15;
+  return g + (r >> 2) * 16 + t * 4 + (r & 3);
+}
+
+struct Layer {
+  int cin = 0, cout = 0, ctot = 0, taps = 9, cfg = CFG_R128_P128;
+  void* w = nullptr;   // packed [ctot][taps*cin] element type
+  float* b = nullptr;  // [ctot] natural order
+};
+
+struct Buffers {
+  size_t tA, cat1, cat2, cat3, cat4, p1, p2, p3, p4, bnb, tB, total;  // byte offsets
+};
+
+}  // namespace
+
+struct unet_handle {
+  unet_config cfg{};
+  DType dt = DType::BF16;
+  float* w0 = nullptr;  // first conv folded fp32 [64][C][3][3]
+  float* b0 = nullptr;
+  Layer L[17];          // d1b d2a d2b d3a d3b d4a d4b bna bnb c4a c4b c3a c3b c2a c2b c1a c1b
+  Layer U[4];           // up4 up3 up2 up1
+  float* head_w = nullptr;
+  float* head_b = nullptr;
+  void* zero = nullptr;
+  bool loaded = false;
+  char* ws = nullptr;
+  size_t ws_bytes = 0;
+  int lastN = 0, lastH = 0, lastW = 0;
+  std::vector<void*> allocs;
+};
+
+namespace {
+
+enum LayerId { D1B, D2A, D2B, D3A, D3B, D4A, D4B, BNA, BNB, C4A, C4B, C3A, C3B, C2A, C2B, C1A, C1B };
+const char* kLayerKey[17][2] = {  // (block, conv index) of each implicit-GEMM 3x3 conv
+    {"down1", "3"}, {"down2", "0"}, {"down2", "3"}, {"down3", "0"}, {"down3", "3"},
+    {"down4", "0"}, {"down4", "3"}, {"bottleneck", "0"}, {"bottleneck", "3"},
+    {"conv4", "0"}, {"conv4", "3"}, {"conv3", "0"}, {"conv3", "3"},
+    {"conv2", "0"}, {"conv2", "3"}, {"conv1", "0"}, {"conv1", "3"}};
+const int kLayerCh[17][2] = {{64, 64},    {64, 128},   {128, 128}, {128, 256}, {256, 256},
+                             {256, 512},  {512, 512},  {512, 1024}, {1024, 1024},
+                             {1024, 512}, {512, 512},  {512, 256}, {256, 256},
+                             {256, 128},  {128, 128},  {128, 64},  {64, 64}};
+const char* kUpKey[4] = {"up4", "up3", "up2", "up1"};
+const int kUpCh[4][2] = {{1024, 512}, {512, 256}, {256, 128}, {128, 64}};
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+Buffers plan(DType dt, int N, int H, int W) {
+  const size_t e = dtype_size(dt);
+  const size_t P = (size_t)N * H * W;  // full-resolution pixels
+  Buffers b{};
+  size_t o = 0;
+  auto take = [&](size_t elems) { size_t r = o; o = align256(o + elems * e); return r; };
+  b.tA = take(P * 64);
+  b.cat1 = take(P * 128);
+  b.cat2 = take(P / 4 * 256);
+  b.cat3 = take(P / 16 * 512);
+  b.cat4 = take(P / 64 * 1024);
+  b.p1 = take(P / 4 * 64);
+  b.p2 = take(P / 16 * 128);
+  b.p3 = take(P / 64 * 256);
+  b.p4 = take(P / 256 * 512);
+  b.bnb = take(P / 256 * 1024);
+  b.tB = take(P / 4 * 128);
+  b.total = o;
+  return b;
+}
+
+int dev_alloc(unet_handle* h, void** p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return fail(UNET_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  h->allocs.push_back(*p);
+  return UNET_OK;
+}
+
+int upload(unet_handle* h, void** dst, const void* src, size_t bytes) {
+  int rc = dev_alloc(h, dst, bytes);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+  return UNET_OK;
+}
+
+struct SD {
+  std::map<std::string, const unet_tensor_view*> m;
+  const float* get(const std::string& k, std::initializer_list<int64_t> shape, std::string& err) const {
+    auto it = m.find(k);
+    if (it == m.end()) { err = "missing key " + k; return nullptr; }
+    const unet_tensor_view* v = it->second;
+    if (v->dtype != 0) { err = "key " + k + " must be float32"; return nullptr; }
+    if ((size_t)v->ndim != shape.size()) { err = "key " + k + ": wrong rank"; return nullptr; }
+    int i = 0;
+    for (int64_t s : shape) {
+      if (v->shape[i++] != s) { err = "key " + k + ": wrong shape"; return nullptr; }
+    }
+    return static_cast<const float*>(v->data);
+  }
+};
+
+// Fold eval BatchNorm into conv (double precision): W' = W*g/sqrt(v+eps), b' = (b-m)*g/sqrt(v+eps)+beta
+int fold(const SD& sd, const std::string& blk, const std::string& ci, int cin, int cout,
+         std::vector<double>& w, std::vector<double>& b) {
+  std::string err;
+  const std::string bn = std::to_string(std::stoi(ci) + 1);
+  const float* W = sd.get(blk + ".net." + ci + ".weight", {cout, cin, 3, 3}, err);
+  const float* B = W ? sd.get(blk + ".net." + ci + ".bias", {cout}, err) : nullptr;
+  const float* g = B ? sd.get(blk + ".net." + bn + ".weight", {cout}, err) : nullptr;
+  const float* be = g ? sd.get(blk + ".net." + bn + ".bias", {cout}, err) : nullptr;
+  const float* mu = be ? sd.get(blk + ".net." + bn + ".running_mean", {cout}, err) : nullptr;
+  const float* var = mu ? sd.get(blk + ".net." + bn + ".running_var", {cout}, err) : nullptr;
+  if (!var) return fail(UNET_EKEY, err);
+  if (!sd.m.count(blk + ".net." + bn + ".num_batches_tracked"))
+    return fail(UNET_EKEY, "missing key " + blk + ".net." + bn + ".num_batches_tracked");
+  w.assign((size_t)cout * cin * 9, 0.0);
+  b.assign(cout, 0.0);
+  for (int o = 0; o < cout; ++o) {
+    const double s = (double)g[o] / std::sqrt((double)var[o] + 1e-5);
+    for (int k = 0; k < cin * 9; ++k) w[(size_t)o * cin * 9 + k] = (double)W[(size_t)o * cin * 9 + k] * s;
+    b[o] = ((double)B[o] - (double)mu[o]) * s + (double)be[o];
+  }
+  return UNET_OK;
+}
+
+void put_elem(DType dt, std::vector<uint8_t>& buf, size_t idx, double v) {
+  if (dt == DType::F32) {
+    float f = (float)v;
+    std::memcpy(&buf[idx * 4], &f, 4);
+  } else {
+    uint16_t u = dt == DType::BF16 ? f32_to_bf16((float)v) : f32_to_f16((float)v);
+    std::memcpy(&buf[idx * 2], &u, 2);
+  }
+}
+
+// 3x3 layer: packed[rho][tap*cin + c] = W'[nat(rho)][c][ky][kx], tap = ky*3+kx
+int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::vector<double>& b) {
+  const int K = 9 * L.cin;
+  std::vector<uint8_t> buf((size_t)L.cout * K * dtype_size(h->dt));
+  for (int rho = 0; rho < L.cout; ++rho) {
+    const int o = natural_of_packed(rho);
+    for (int tap = 0; tap < 9; ++tap)
+      for (int c = 0; c < L.cin; ++c)
+        put_elem(h->dt, buf, (size_t)rho * K + (size_t)tap * L.cin + c, w[((size_t)o * L.cin + c) * 9 + tap]);
+  }
+  std::vector<float> bf(b.begin(), b.end());
+  int rc = upload(h, &L.w, buf.data(), buf.size());
+  if (!rc) rc = upload(h, (void**)&L.b, bf.data(), bf.size() * 4);
+  return rc;
+}
+
+// ConvTranspose2d(k2,s2): natural GEMM row R = (a*2+b)*cout + o; packed[rho][c] = W[c][o][a][b]
+int packT(unet_handle* h, Layer& L, const float* W, const float* B) {
+  const int R = 4 * L.cout;
+  std::vector<uint8_t> buf((size_t)R * L.cin * dtype_size(h->dt));
+  for (int rho = 0; rho < R; ++rho) {
+    const int nat = natural_of_packed(rho);
+    const int ab = nat / L.cout, o = nat % L.cout;
+    for (int c = 0; c < L.cin; ++c)
+      put_elem(h->dt, buf, (size_t)rho * L.cin + c, W[(((size_t)c * L.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]);
+  }
+  std::vector<float> bias(R);
+  for (int r = 0; r < R; ++r) bias[r] = B[r % L.cout];
+  int rc = upload(h, &L.w, buf.data(), buf.size());
+  if (!rc) rc = upload(h, (void**)&L.b, bias.data(), bias.size() * 4);
+  return rc;
+}
+
+void free_all(unet_handle* h) {
+  for (void* p : h->allocs) (void)hipFree(p);
+  h->allocs.clear();
+  if (h->ws) (void)hipFree(h->ws);
+  h->ws = nullptr;
+  h->ws_bytes = 0;
+}
+
+int check_geometry(const unet_handle* h, int N, int H, int W) {
+  if (N <= 0 || H <= 0 || W <= 0) return fail(UNET_EINVAL, "N, H, W must be positive");
+  if (H % 16 || W % 16)
+    return fail(UNET_ESHAPE, "H and W must be divisible by 16 (4 pooling levels; the reference "
+                             "fails in torch.cat otherwise, unet_model.py:71)");
+  if ((long long)N * H * W > (1LL << 31) / 2) return fail(UNET_ESHAPE, "N*H*W too large for one call");
+  (void)h;
+  return UNET_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* unet_last_error(void) { return g_err.c_str(); }
+int unet_abi_version(void) { return UNET_ABI_VERSION; }
+
+int unet_create(const unet_config* cfg, unet_handle** out) {
+  if (!cfg || !out) return fail(UNET_EINVAL, "null argument");
+  if (cfg->n_channels != 1 && cfg->n_channels != 3) return fail(UNET_EINVAL, "n_channels must be 1 or 3");
+  if (cfg->n_classes < 1 || cfg->n_classes > kMaxClasses) return fail(UNET_EINVAL, "n_classes must be 1..4");
+  if (cfg->dtype < 0 || cfg->dtype > 2) return fail(UNET_EINVAL, "bad dtype");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(UNET_EINVAL, "bad device ordinal");
+  unet_handle* h = new unet_handle();
+  h->cfg = *cfg;
+  h->dt = (DType)cfg->dtype;
+  for (int i = 0; i < 17; ++i) {
+    h->L[i].cin = kLayerCh[i][0];
+    h->L[i].cout = h->L[i].ctot = kLayerCh[i][1];
+    h->L[i].taps = 9;
+    h->L[i].cfg = h->L[i].cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
+  }
+  h->L[C1B].cfg = CFG_R64_P128;
+  for (int i = 0; i < 4; ++i) {
+    h->U[i].cin = kUpCh[i][0];
+    h->U[i].cout = kUpCh[i][1];
+    h->U[i].ctot = 4 * kUpCh[i][1];
+    h->U[i].taps = 1;
+    h->U[i].cfg = CFG_R128_P128;
+  }
+  DeviceGuard g(cfg->device);
+  std::vector<uint8_t> z(256, 0);
+  int rc = upload(h, &h->zero, z.data(), z.size());
+  if (rc) { free_all(h); delete h; return rc; }
+  *out = h;
+  return UNET_OK;
+}
+
+int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
+  if (!h || (!t && n)) return fail(UNET_EINVAL, "null argument");
+  SD sd;
+  for (int i = 0; i < n; ++i) {
+    if (!t[i].name) return fail(UNET_EINVAL, "tensor without a name");
+    sd.m[t[i].name] = &t[i];
+  }
+  // strict: exactly the reference key set (136 keys for the reference widths)
+  const int expected = 9 * 14 + 4 * 2 + 2;
+  if ((int)sd.m.size() != expected)
+    return fail(UNET_EKEY, "state_dict has " + std::to_string(sd.m.size()) + " keys, expected " +
+                               std::to_string(expected));
+  DeviceGuard g(h->cfg.device);
+  // drop previously loaded weights (keep the zero page)
+  for (void* p : h->allocs)
+    if (p != h->zero) (void)hipFree(p);
+  h->allocs.assign(1, h->zero);
+  h->loaded = false;
+
+  std::vector<double> w, b;
+  const int C = h->cfg.n_channels;
+  int rc = fold(sd, "down1", "0", C, 64, w, b);
+  if (rc) return rc;
+  {
+    std::vector<float> wf(w.begin(), w.end()), bf(b.begin(), b.end());
+    rc = upload(h, (void**)&h->w0, wf.data(), wf.size() * 4);
+    if (!rc) rc = upload(h, (void**)&h->b0, bf.data(), bf.size() * 4);
+    if (rc) return rc;
+  }
+  for (int i = 0; i < 17; ++i) {
+    rc = fold(sd, kLayerKey[i][0], kLayerKey[i][1], h->L[i].cin, h->L[i].cout, w, b);
+    if (!rc) rc = pack3x3(h, h->L[i], w, b);
+    if (rc) return rc;
+  }
+  std::string err;
+  for (int i = 0; i < 4; ++i) {
+    const Layer& L = h->U[i];
+    const float* W = sd.get(std::string(kUpKey[i]) + ".weight", {L.cin, L.cout, 2, 2}, err);
+    const float* B = W ? sd.get(std::string(kUpKey[i]) + ".bias", {L.cout}, err) : nullptr;
+    if (!B) return fail(UNET_EKEY, err);
+    rc = packT(h, h->U[i], W, B);
+    if (rc) return rc;
+  }
+  const int ncls = h->cfg.n_classes;
+  const float* HW = sd.get("out_conv.weight", {ncls, 64, 1, 1}, err);
+  const float* HB = HW ? sd.get("out_conv.bias", {ncls}, err) : nullptr;
+  if (!HB) return fail(UNET_EKEY, err);
+  rc = upload(h, (void**)&h->head_w, HW, (size_t)ncls * 64 * 4);
+  if (!rc) rc = upload(h, (void**)&h->head_b, HB, (size_t)ncls * 4);
+  if (rc) return rc;
+  h->loaded = true;
+  return UNET_OK;
+}
+
+size_t unet_workspace_bytes(const unet_handle* h, int N, int H, int W) {
+  if (!h || N <= 0 || H <= 0 || W <= 0) return 0;
+  return plan(h->dt, N, H, W).total;
+}
+
+int unet_reserve(unet_handle* h, int N, int H, int W) {
+  if (!h) return fail(UNET_EINVAL, "null handle");
+  int rc = check_geometry(h, N, H, W);
+  if (rc) return rc;
+  const size_t need = plan(h->dt, N, H, W).total;
+  if (need <= h->ws_bytes) return UNET_OK;
+  DeviceGuard g(h->cfg.device);
+  if (h->ws) {
+    HIP_TRY(hipDeviceSynchronize());
+    (void)hipFree(h->ws);
+    h->ws = nullptr;
+    h->ws_bytes = 0;
+  }
+  hipError_t e = hipMalloc((void**)&h->ws, need);
+  if (e != hipSuccess) {
+    h->ws = nullptr;
+    return fail(UNET_ENOMEM, std::string("workspace hipMalloc: ") + hipGetErrorString(e));
+  }
+  h->ws_bytes = need;
+  return UNET_OK;
+}
+
+namespace {
+
+int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, int H, int W, int ldi,
+              void* out, int ldo, int out_off, void* out2, int ldo2, hipStream_t s,
+              float* logits = nullptr, void* masks = nullptr, int mask_kind = MASK_NONE) {
+  IgemmArgs a{};
+  a.in = in;
+  a.wgt = L.w;
+  a.bias = L.b;
+  a.zero = h->zero;
+  a.out = out;
+  a.out2 = out2;
+  a.head_w = h->head_w;
+  a.head_b = h->head_b;
+  a.logits = logits;
+  a.masks = static_cast<uint8_t*>(masks);
+  a.N = N; a.H = H; a.W = W;
+  a.Cin = L.cin; a.ldi = ldi;
+  a.Ctot = L.ctot; a.Cout = L.cout;
+  a.ldo = ldo; a.out_off = out_off; a.ldo2 = ldo2;
+  a.ncls = h->cfg.n_classes;
+  a.mask_kind = mask_kind;
+  for (int i = 0; i < kMaxClasses; ++i) a.thr[i] = h->cfg.thresholds[i];
+  const int BR = cfg_rows(L.cfg), BP = cfg_pixels(L.cfg);
+  const int TH = BP / 16;
+  a.tiles_x = (W + 15) / 16;
+  a.tiles_y = (H + TH - 1) / TH;
+  a.n_ct = L.ctot / BR;
+  const long long nb = (long long)N * a.tiles_x * a.tiles_y * a.n_ct;
+  if (nb <= 0 || nb > 0x7FFFFFFFLL) return fail(UNET_ESHAPE, "grid too large");
+  a.n_blocks = (int)nb;
+  hipError_t e = launch_igemm(h->dt, L.cfg, L.taps, epi, a, s);
+  if (e != hipSuccess) return fail(UNET_EHIP, std::string("igemm launch: ") + hipGetErrorString(e));
+  return UNET_OK;
+}
+
+}  // namespace
+
+namespace {
+// The launch sequence of UNet.forward (unet_model.py:55-86).  ev (optional, kLaunches+1
+// events) brackets every launch for per-layer timing.
+int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
+                 int mask_kind, int N, int H, int W, void* stream, hipEvent_t* ev) {
+  if (!h || !x) return fail(UNET_EINVAL, "null argument");
+  if (!h->loaded) return fail(UNET_ESTATE, "weights not loaded");
+  if (x_layout != UNET_LAYOUT_NCHW || x_dtype != UNET_IN_F32)
+    return fail(UNET_EINVAL, "only fp32 NCHW input is supported");
+  if (mask_kind < 0 || mask_kind > 2) return fail(UNET_EINVAL, "bad mask_kind");
+  if (mask_kind != UNET_MASK_NONE && !masks) return fail(UNET_EINVAL, "mask_kind set but masks is NULL");
+  int rc = check_geometry(h, N, H, W);
+  if (rc) return rc;
+  rc = unet_reserve(h, N, H, W);
+  if (rc) return rc;
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Buffers B = plan(h->dt, N, H, W);
+  char* ws = h->ws;
+  auto buf = [&](size_t off) { return static_cast<void*>(ws + off); };
+  const int H2 = H / 2, W2 = W / 2, H4 = H / 4, W4 = W / 4, H8 = H / 8, W8 = W / 8, H16 = H / 16, W16 = W / 16;
+
+  // down1.net.0 (C -> 64): direct conv
+  FirstConvArgs f{};
+  f.x = static_cast<const float*>(x);
+  f.w = h->w0;
+  f.b = h->b0;
+  f.out = buf(B.tA);
+  f.N = N; f.C = h->cfg.n_channels; f.H = H; f.W = W;
+  int li = 0;
+  auto mark = [&]() { if (ev) (void)hipEventRecord(ev[li], s); ++li; };
+  mark();
+  hipError_t e = launch_first_conv(h->dt, f, s);
+  if (e != hipSuccess) return fail(UNET_EHIP, std::string("first conv launch: ") + hipGetErrorString(e));
+
+#define RUN(...) do { mark(); rc = run_igemm(__VA_ARGS__); if (rc) return rc; } while (0)
+  // encoder: conv b of each level writes the skip into the upper half of the concat
+  // buffer (torch.cat([up, skip]) puts skip second, unet_model.py:71) and the pooled map.
+  RUN(h, h->L[D1B], EPI_POOL, buf(B.tA), N, H, W, 64, buf(B.cat1), 128, 64, buf(B.p1), 64, s);
+  RUN(h, h->L[D2A], EPI_STORE, buf(B.p1), N, H2, W2, 64, buf(B.tA), 128, 0, nullptr, 0, s);
+  RUN(h, h->L[D2B], EPI_POOL, buf(B.tA), N, H2, W2, 128, buf(B.cat2), 256, 128, buf(B.p2), 128, s);
+  RUN(h, h->L[D3A], EPI_STORE, buf(B.p2), N, H4, W4, 128, buf(B.tA), 256, 0, nullptr, 0, s);
+  RUN(h, h->L[D3B], EPI_POOL, buf(B.tA), N, H4, W4, 256, buf(B.cat3), 512, 256, buf(B.p3), 256, s);
+  RUN(h, h->L[D4A], EPI_STORE, buf(B.p3), N, H8, W8, 256, buf(B.tA), 512, 0, nullptr, 0, s);
+  RUN(h, h->L[D4B], EPI_POOL, buf(B.tA), N, H8, W8, 512, buf(B.cat4), 1024, 512, buf(B.p4), 512, s);
+  RUN(h, h->L[BNA], EPI_STORE, buf(B.p4), N, H16, W16, 512, buf(B.tA), 1024, 0, nullptr, 0, s);
+  RUN(h, h->L[BNB], EPI_STORE, buf(B.tA), N, H16, W16, 1024, buf(B.bnb), 1024, 0, nullptr, 0, s);
+  // decoder: up_k writes the lower half of the concat buffer, conv_k reads all of it
+  RUN(h, h->U[0], EPI_UPSCATTER, buf(B.bnb), N, H16, W16, 1024, buf(B.cat4), 1024, 0, nullptr, 0, s);
+  RUN(h, h->L[C4A], EPI_STORE, buf(B.cat4), N, H8, W8, 1024, buf(B.tA), 512, 0, nullptr, 0, s);
+  RUN(h, h->L[C4B], EPI_STORE, buf(B.tA), N, H8, W8, 512, buf(B.tB), 512, 0, nullptr, 0, s);
+  RUN(h, h->U[1], EPI_UPSCATTER, buf(B.tB), N, H8, W8, 512, buf(B.cat3), 512, 0, nullptr, 0, s);
+  RUN(h, h->L[C3A], EPI_STORE, buf(B.cat3), N, H4, W4, 512, buf(B.tA), 256, 0, nullptr, 0, s);
+  RUN(h, h->L[C3B], EPI_STORE, buf(B.tA), N, H4, W4, 256, buf(B.tB), 256, 0, nullptr, 0, s);
+  RUN(h, h->U[2], EPI_UPSCATTER, buf(B.tB), N, H4, W4, 256, buf(B.cat2), 256, 0, nullptr, 0, s);
+  RUN(h, h->L[C2A], EPI_STORE, buf(B.cat2), N, H2, W2, 256, buf(B.tA), 128, 0, nullptr, 0, s);
+  RUN(h, h->L[C2B], EPI_STORE, buf(B.tA), N, H2, W2, 128, buf(B.tB), 128, 0, nullptr, 0, s);
+  RUN(h, h->U[3], EPI_UPSCATTER, buf(B.tB), N, H2, W2, 128, buf(B.cat1), 128, 0, nullptr, 0, s);
+  RUN(h, h->L[C1A], EPI_STORE, buf(B.cat1), N, H, W, 128, buf(B.tA), 64, 0, nullptr, 0, s);
+  // conv1.net.3 + BN + ReLU + out_conv (1x1) + sigmoid/threshold, one launch
+  RUN(h, h->L[C1B], EPI_HEAD, buf(B.tA), N, H, W, 64, nullptr, 0, 0, nullptr, 0, s,
+      static_cast<float*>(logits), masks, mask_kind);
+#undef RUN
+  mark();
+  h->lastN = N; h->lastH = H; h->lastW = W;
+  return UNET_OK;
+}
+}  // namespace
+
+int unet_forward(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
+                 int mask_kind, int N, int H, int W, void* stream) {
+  return forward_impl(h, x, x_layout, x_dtype, logits, masks, mask_kind, N, H, W, stream, nullptr);
+}
+
+int unet_num_launches(void) { return UNET_NUM_LAUNCHES; }
+
+int unet_forward_timed(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
+                       int mask_kind, int N, int H, int W, void* stream, float* launch_ms) {
+  if (!h || !launch_ms) return fail(UNET_EINVAL, "null argument");
+  DeviceGuard g(h->cfg.device);
+  hipEvent_t ev[UNET_NUM_LAUNCHES + 1];
+  for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+  int rc = forward_impl(h, x, x_layout, x_dtype, logits, masks, mask_kind, N, H, W, stream, ev);
+  if (!rc) {
+    HIP_TRY(hipEventSynchronize(ev[UNET_NUM_LAUNCHES]));
+    for (int i = 0; i < UNET_NUM_LAUNCHES; ++i) HIP_TRY(hipEventElapsedTime(&launch_ms[i], ev[i], ev[i + 1]));
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return rc;
+}
+
+int unet_debug_fetch(unet_handle* h, const char* name, float* dst, size_t* numel, void* stream) {
+  if (!h || !name) return fail(UNET_EINVAL, "null argument");
+  if (!h->lastN) return fail(UNET_ESTATE, "no forward has run");
+  const int N = h->lastN, H = h->lastH, W = h->lastW;
+  const Buffers B = plan(h->dt, N, H, W);
+  struct Src { size_t off; int div, C, ld, choff; };
+  static const std::map<std::string, int> idx = {
+      {"c1", 0}, {"p1", 1}, {"c2", 2}, {"p2", 3}, {"c3", 4}, {"p3", 5}, {"c4", 6}, {"p4", 7},
+      {"bn", 8}, {"c7", 9}, {"u1", 10}, {"u2", 11}, {"u3", 12}, {"u4", 13}, {"c8a", 14}};
+  auto it = idx.find(name);
+  if (it == idx.end()) return fail(UNET_EINVAL, std::string("unknown intermediate ") + name);
+  const Src table[] = {{B.cat1, 1, 64, 128, 64},   {B.p1, 2, 64, 64, 0},     {B.cat2, 2, 128, 256, 128},
+                       {B.p2, 4, 128, 128, 0},     {B.cat3, 4, 256, 512, 256}, {B.p3, 8, 256, 256, 0},
+                       {B.cat4, 8, 512, 1024, 512}, {B.p4, 16, 512, 512, 0},  {B.bnb, 16, 1024, 1024, 0},
+                       {B.tB, 2, 128, 128, 0},     {B.cat1, 1, 64, 128, 0},  {B.cat2, 2, 128, 256, 0},
+                       {B.cat3, 4, 256, 512, 0},   {B.cat4, 8, 512, 1024, 0}, {B.tA, 1, 64, 64, 0}};
+  const Src& t = table[it->second];
+  const int h_ = H / t.div, w_ = W / t.div;
+  const size_t cnt = (size_t)N * t.C * h_ * w_;
+  if (numel) *numel = cnt;
+  if (!dst) return UNET_OK;
+  DeviceGuard g(h->cfg.device);
+  hipError_t e = launch_nhwc_to_nchw_f32(h->dt, h->ws + t.off, N, h_, w_, t.C, t.ld, t.choff, dst,
+                                         static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail(UNET_EHIP, std::string("debug fetch: ") + hipGetErrorString(e));
+  return UNET_OK;
+}
+
+int unet_destroy(unet_handle* h) {
+  if (!h) return UNET_OK;
+  {
+    DeviceGuard g(h->cfg.device);
+    (void)hipDeviceSynchronize();
+    free_all(h);
+  }
+  delete h;
+  return UNET_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// Internal (non-ABI) declarations shared by the HIP kernels and the C-ABI host layer.
+// Nothing here crosses the library boundary; see include/unet_mi355x.h for that.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+
+namespace unet {
+
+enum class DType : int { F32 = 0, BF16 = 1, F16 = 2 };
+
+inline size_t dtype_size(DType t) { return t == DType::F32 ? 4 : 2; }
+
+// Epilogue kinds of the implicit-GEMM kernel.
+enum Epi : int {
+  EPI_STORE = 0,    // bias + ReLU -> NHWC store (conv3x3 + folded BN + ReLU)
+  EPI_POOL = 1,     // EPI_STORE + fused 2x2/2 max-pool into a second NHWC tensor
+  EPI_HEAD = 2,     // bias + ReLU kept in fp32 -> fused 1x1 out_conv -> logits / masks
+  EPI_UPSCATTER = 3 // ConvTranspose2d(k2,s2): bias, no ReLU, pixel-shuffle store
+};
+
+// Mask output formats for EPI_HEAD.
+enum MaskKind : int { MASK_NONE = 0, MASK_U8 = 1, MASK_BITS = 2 };
+
+constexpr int kMaxClasses = 4;
+
+// One implicit-GEMM launch.  GEMM view: rows = output channels (A = packed
+// weights [Ctot][K]), columns = pixels (B = gathered NHWC activations),
+// K = TAPS * Cin ordered (tap, cin).
+struct IgemmArgs {
+  const void* in;      // NHWC activations (element type T), pixel stride ldi
+  const void* wgt;     // packed weights [Ctot][TAPS*Cin], rows permuted in 64-row groups
+  const float* bias;   // [Ctot] natural row order (BN folded)
+  const void* zero;    // >= 256 zero bytes (source of the conv zero padding)
+  void* out;           // NHWC output, pixel stride ldo, channel offset out_off
+  void* out2;          // EPI_POOL: pooled NHWC output (pixel stride ldo2)
+  const float* head_w; // EPI_HEAD: [ncls][64] fp32
+  const float* head_b; // EPI_HEAD: [ncls]
+  float* logits;       // EPI_HEAD: NCHW fp32 logits or nullptr
+  uint8_t* masks;      // EPI_HEAD: masks or nullptr
+  int N, H, W;         // input spatial dims (3x3: == output dims; convT: output is 2H x 2W)
+  int Cin, ldi;
+  int Ctot;            // GEMM rows (Cout, or 4*Cout for convT)
+  int Cout;            // convT: channels per (a,b) group
+  int ldo, out_off, ldo2;
+  int ncls, mask_kind;
+  float thr[kMaxClasses];
+  int tiles_x, tiles_y, n_ct, n_blocks;
+};
+
+struct FirstConvArgs {
+  const float* x;      // NCHW fp32 input [N][C][H][W]
+  const float* w;      // [64][C][3][3] folded
+  const float* b;      // [64] folded
+  void* out;           // NHWC [N][H][W][64] element type T
+  int N, C, H, W;
+};
+
+// Kernel configurations (rows tile x pixel tile).
+enum Cfg : int { CFG_R128_P128 = 0, CFG_R64_P128 = 1, CFG_R64_P256 = 2, CFG_R128_P256 = 3 };
+int cfg_rows(int cfg);
+int cfg_pixels(int cfg);
+
+hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s);
+hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s);
+// NHWC (pixel stride ld, channel offset choff, C channels) element type t -> NCHW fp32
+hipError_t launch_nhwc_to_nchw_f32(DType t, const void* src, int N, int H, int W, int C, int ld,
+                                   int choff, float* dst, hipStream_t s);
+
+}  // namespace unet

@@ -1,0 +1,462 @@
+// HIP kernels for the UNet forward path on MI355X (gfx950 / CDNA4).
+//
+// Reference semantics: unet_model.py:6-86 (DoubleConv = conv3x3 -> BN(eval) -> ReLU
+// twice; MaxPool2d(2); ConvTranspose2d(k2, s2); torch.cat([up, skip], 1); 1x1 out_conv).
+//
+// Design:
+//  * activations are NHWC in HBM (bf16 / f16 / f32), so one pixel's channel run is a
+//    contiguous 128-byte row of a GEMM operand;
+//  * every 3x3 conv, the ConvTranspose2d and the fused 1x1 head run through ONE
+//    implicit-GEMM kernel: rows = output channels (A = pre-packed, BN-folded weights),
+//    columns = output pixels (B = the shifted NHWC input gathered per tap),
+//    K = (tap, cin).  Tiles are staged global -> LDS with global_load_lds_dwordx4
+//    (LDS-DMA, no VGPR round trip); conv zero padding comes from a zero page so the
+//    DMA never needs a mask; the LDS image is XOR-swizzled through the per-lane
+//    source address (lane-linear destination) so the ds_read_b128 fragment reads are
+//    bank-conflict free;
+//  * MFMA v_mfma_f32_16x16x32_{bf16,f16} (f32: v_mfma_f32_16x16x4_f32, exact fp32);
+//  * epilogues: bias (BN folded) + ReLU; fused 2x2 max-pool (the skip tensor and
+//    the pooled tensor are written by the same launch); fused 64->ncls 1x1 head with
+//    sigmoid/threshold masks; ConvTranspose pixel-shuffle scatter.  torch.cat is
+//    zero-copy: producers write straight into channel halves of one NHWC buffer.
+#include "unet_internal.h"
+
+namespace unet {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+int cfg_rows(int cfg) { return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256) ? 128 : 64; }
+int cfg_pixels(int cfg) { return (cfg == CFG_R64_P256 || cfg == CFG_R128_P256) ? 256 : 128; }
+
+// ---------------------------------------------------------------------------------
+// element traits
+// ---------------------------------------------------------------------------------
+template <typename T> struct Elem;
+template <> struct Elem<float> { static constexpr int BKE = 32; };   // 32 f32 = 128 B
+template <> struct Elem<__bf16> { static constexpr int BKE = 64; };  // 64 bf16 = 128 B
+template <> struct Elem<_Float16> { static constexpr int BKE = 64; };
+
+template <typename T>
+__device__ __forceinline__ void mfma_frag(f32x4& acc, const uint4& a, const uint4& b);
+
+template <>
+__device__ __forceinline__ void mfma_frag<__bf16>(f32x4& acc, const uint4& a, const uint4& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ void mfma_frag<_Float16>(f32x4& acc, const uint4& a, const uint4& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                               __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
+}
+// f32: the 16-byte fragment holds 4 consecutive k of one row; four 16x16x4 MFMAs, the
+// e-th one taking element e of every lane.  A and B read the same (row, chunk) map, so
+// this is the same dot product in a permuted (exact fp32 fma-chain) order.
+template <>
+__device__ __forceinline__ void mfma_frag<float>(f32x4& acc, const uint4& a, const uint4& b) {
+  const f32x4 av = __builtin_bit_cast(f32x4, a);
+  const f32x4 bv = __builtin_bit_cast(f32x4, b);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], acc, 0, 0, 0);
+}
+
+// store 16 consecutive channels (fp32 values) as element type T (16-byte vector stores)
+template <typename T>
+__device__ __forceinline__ void store16(T* dst, const float (&v)[16]);
+template <>
+__device__ __forceinline__ void store16<float>(float* dst, const float (&v)[16]) {
+  f32x4* d = reinterpret_cast<f32x4*>(dst);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+}
+template <>
+__device__ __forceinline__ void store16<__bf16>(__bf16* dst, const float (&v)[16]) {
+  bf16x8 lo, hi;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { lo[i] = (__bf16)v[i]; hi[i] = (__bf16)v[8 + i]; }
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = __builtin_bit_cast(uint4, lo);
+  d[1] = __builtin_bit_cast(uint4, hi);
+}
+template <>
+__device__ __forceinline__ void store16<_Float16>(_Float16* dst, const float (&v)[16]) {
+  f16x8 lo, hi;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { lo[i] = (_Float16)v[i]; hi[i] = (_Float16)v[8 + i]; }
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = __builtin_bit_cast(uint4, lo);
+  d[1] = __builtin_bit_cast(uint4, hi);
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_dst, 16, 0, 0);
+}
+
+// Pixel p (0..BP-1) of a block tile -> (row, col) inside the TH x 16 tile.  Pixels come
+// in groups of 16 = 2 rows x 8 columns, so an MFMA column group (lane & 15) covers whole
+// 2x2 pooling windows: partners are lanes ^1 and ^8.
+__device__ __forceinline__ void pix_of(int p, int& py, int& px) {
+  const int g = p >> 4, j = p & 15;
+  py = 2 * (g >> 1) + (j >> 3);
+  px = 8 * (g & 1) + (j & 7);
+}
+
+// ---------------------------------------------------------------------------------
+// implicit-GEMM kernel
+// ---------------------------------------------------------------------------------
+// WR waves along rows (64 rows each, 4 MFMA row tiles), WPX waves along pixels
+// (TP MFMA column tiles of 16 pixels each).  4 waves per block.
+template <typename T, int WR, int WPX, int TP, int TAPS, int EPI>
+__global__ __launch_bounds__(256, 2) void igemm_kernel(const IgemmArgs a) {
+  static_assert(WR * WPX == 4, "4 waves per block");
+  constexpr int TC = 4;
+  constexpr int BR = WR * 64;
+  constexpr int BP = WPX * TP * 16;
+  constexpr int TH = BP / 16;
+  constexpr int BKE = Elem<T>::BKE;
+  constexpr int STAGE = (BR + BP) * 128;
+  constexpr int A_INS = BR / 32;  // glds instructions per wave for the A tile
+  constexpr int B_INS = BP / 32;  // ... for the B tile
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wr = wave / WPX;
+  const int wp = wave % WPX;
+
+  // XCD-aware bijective remap: hardware deals blocks round-robin over 8 XCDs; give each
+  // XCD a contiguous range so that the n_ct row tiles of one pixel tile (which share the
+  // gathered activations) run on one L2.
+  int lid;
+  {
+    const int nb = a.n_blocks, q = nb >> 3, r = nb & 7;
+    const int bid = blockIdx.x, x = bid & 7, k = bid >> 3;
+    lid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  }
+  const int ct = lid % a.n_ct;
+  int mt = lid / a.n_ct;
+  const int tx = mt % a.tiles_x;
+  mt /= a.tiles_x;
+  const int ty = mt % a.tiles_y;
+  const int n = mt / a.tiles_y;
+
+  const int H = a.H, W = a.W;
+  const int K = TAPS * a.Cin;
+  const int cpt = a.Cin / BKE;  // 128-byte chunks per tap
+  const int S = TAPS * cpt;
+
+  // per-lane source chunk (XOR swizzle through the source address; LDS stays lane-linear)
+  const int src_chunk = (lane & 7) ^ ((lane >> 3) & 7);
+  const char* zero = reinterpret_cast<const char*>(a.zero) + src_chunk * 16;
+
+  // B rows owned by this lane: (oy, ox) of the output pixel and its flattened index
+  int b_oy[B_INS], b_ox[B_INS], b_pix[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = wave * (BP / 4) + j * 8 + (lane >> 3);
+    int py, px;
+    pix_of(row, py, px);
+    b_oy[j] = ty * TH + py;
+    b_ox[j] = tx * 16 + px;
+    b_pix[j] = (n * H + b_oy[j]) * W + b_ox[j];
+  }
+  const char* wsrc[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = wave * (BR / 4) + j * 8 + (lane >> 3);
+    wsrc[j] = reinterpret_cast<const char*>(a.wgt) +
+              ((size_t)(ct * BR + row) * K) * sizeof(T) + src_chunk * 16;
+  }
+  const char* in = reinterpret_cast<const char*>(a.in) + src_chunk * 16;
+
+  auto stage = [&](int s, int buf) {
+    const int tap = s / cpt;
+    const int c0 = (s - tap * cpt) * BKE;
+    char* As = lds + buf * STAGE;
+    char* Bs = As + BR * 128;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j)
+      glds16(wsrc[j] + (size_t)s * BKE * sizeof(T), As + (wave * (BR / 4) + j * 8) * 128);
+    int dy = 0, dx = 0;
+    if (TAPS == 9) { dy = tap / 3 - 1; dx = tap - (tap / 3) * 3 - 1; }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const int iy = b_oy[j] + dy, ix = b_ox[j] + dx;
+      const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W &&
+                      b_oy[j] < H && b_ox[j] < W;
+      const char* src = ok ? in + ((long long)(b_pix[j] + dy * W + dx) * a.ldi + c0) * (long long)sizeof(T)
+                           : zero;
+      glds16(src, Bs + (wave * (BP / 4) + j * 8) * 128);
+    }
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int t = 0; t < TC; ++t)
+#pragma unroll
+    for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int frag_row = lane & 15;
+  for (int s = 0; s < S; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < S) stage(s + 1, buf ^ 1);
+    const char* As = lds + buf * STAGE + (wr * 64 + frag_row) * 128;
+    const char* Bs = lds + buf * STAGE + BR * 128 + (wp * TP * 16 + frag_row) * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int phys = ((kk * 4 + (lane >> 4)) ^ (lane & 7)) * 16;
+      uint4 af[TC], bfv[TP];
+#pragma unroll
+      for (int t = 0; t < TC; ++t) af[t] = *reinterpret_cast<const uint4*>(As + t * 16 * 128 + phys);
+#pragma unroll
+      for (int p = 0; p < TP; ++p) bfv[p] = *reinterpret_cast<const uint4*>(Bs + p * 16 * 128 + phys);
+#pragma unroll
+      for (int t = 0; t < TC; ++t)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) mfma_frag<T>(acc[t][p], af[t], bfv[p]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // Lane holds, for pixel column (lane & 15) of each p tile, the 16 consecutive natural
+  // rows rbase .. rbase+15 (the weight packing permutes rows so that MFMA row
+  // 4*(lane>>4)+e of row-tile t is natural row 16*(lane>>4) + 4*t + e).
+  const int q = lane >> 4;
+  const int col = lane & 15;
+  const int rbase = ct * BR + wr * 64 + q * 16;
+  float bv[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + rbase + 4 * i);
+    bv[4 * i] = b4[0]; bv[4 * i + 1] = b4[1]; bv[4 * i + 2] = b4[2]; bv[4 * i + 3] = b4[3];
+  }
+
+#pragma unroll
+  for (int p = 0; p < TP; ++p) {
+    int py, px;
+    pix_of(wp * TP * 16 + p * 16 + col, py, px);
+    const int oy = ty * TH + py, ox = tx * 16 + px;
+    const bool inside = oy < H && ox < W;
+    float v[16];
+#pragma unroll
+    for (int t = 0; t < TC; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = acc[t][p][e] + bv[t * 4 + e];
+        if (EPI != EPI_UPSCATTER) x = fmaxf(x, 0.f);
+        v[t * 4 + e] = x;
+      }
+
+    if constexpr (EPI == EPI_STORE || EPI == EPI_POOL) {
+      if (inside) {
+        T* dst = reinterpret_cast<T*>(a.out) + ((long long)(n * H + oy) * W + ox) * a.ldo + a.out_off + rbase;
+        store16<T>(dst, v);
+      }
+      if constexpr (EPI == EPI_POOL) {
+        float m[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          float o = fmaxf(v[e], __shfl_xor(v[e], 1));
+          m[e] = fmaxf(o, __shfl_xor(o, 8));
+        }
+        if ((col & 9) == 0 && oy + 1 < H && ox + 1 < W) {
+          const int Ho = H >> 1, Wo = W >> 1;
+          T* dst = reinterpret_cast<T*>(a.out2) +
+                   ((long long)(n * Ho + (oy >> 1)) * Wo + (ox >> 1)) * a.ldo2 + rbase;
+          store16<T>(dst, m);
+        }
+      }
+    } else if constexpr (EPI == EPI_UPSCATTER) {
+      if (inside) {
+        const int ab = rbase / a.Cout;
+        const int o0 = rbase - ab * a.Cout;
+        const int Y = 2 * oy + (ab >> 1), X = 2 * ox + (ab & 1);
+        T* dst = reinterpret_cast<T*>(a.out) +
+                 ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0;
+        store16<T>(dst, v);
+      }
+    } else {  // EPI_HEAD: 1x1 conv 64 -> ncls on the fp32 activations, then masks
+      for (int c = 0; c < a.ncls; ++c) {
+        const float* hw = a.head_w + c * 64 + wr * 64 + q * 16;
+        float sum = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sum = fmaf(hw[e], v[e], sum);
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+        const float logit = sum + a.head_b[c];
+        const long long pix = ((long long)(n * a.ncls + c) * H + oy) * W + ox;
+        if (a.logits && q == 0 && inside) a.logits[pix] = logit;
+        if (a.mask_kind != MASK_NONE) {
+          const float prob = 1.0f / (1.0f + expf(-logit));   // torch.sigmoid, inference.py:72
+          const bool on = prob > a.thr[c];                    // strict '>', inference.py:76-78
+          if (a.mask_kind == MASK_U8) {
+            if (q == 0 && inside) a.masks[pix] = on ? 1 : 0;
+          } else {
+            const unsigned long long bal = __ballot(on);
+            if (q == 0 && (col & 7) == 0 && inside) {
+              const unsigned byte = (unsigned)(bal >> (col & 8)) & 0xFFu;
+              a.masks[((long long)(n * a.ncls + c) * H + oy) * (W >> 3) + (ox >> 3)] = (uint8_t)byte;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// first conv: C in {1,3} input channels, fp32 NCHW in, 64 channels NHWC out.
+// K = 9*C is far too short for MFMA; it is a VALU direct conv, bound by HBM
+// (read 4*C B + write 64*sizeof(T) B per pixel).
+// ---------------------------------------------------------------------------------
+template <typename T, int C>
+__global__ __launch_bounds__(256) void first_conv_kernel(const FirstConvArgs a) {
+  constexpr int KW = 9 * C;
+  __shared__ float ws[64 * KW];
+  __shared__ float bs[64];
+  for (int i = threadIdx.x; i < 64 * KW; i += 256) ws[i] = a.w[i];
+  if (threadIdx.x < 64) bs[threadIdx.x] = a.b[threadIdx.x];
+  __syncthreads();
+  const long long total = (long long)a.N * a.H * a.W;
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= total) return;
+  const int x = (int)(pix % a.W);
+  const long long t = pix / a.W;
+  const int y = (int)(t % a.H);
+  const int n = (int)(t / a.H);
+  float xin[KW];
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int iy = y + ky - 1, ix = x + kx - 1;
+        const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+        xin[(c * 3 + ky) * 3 + kx] = ok ? a.x[(((long long)n * C + c) * a.H + iy) * a.W + ix] : 0.f;
+      }
+  T* dst = reinterpret_cast<T*>(a.out) + pix * 64;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int co = g * 16 + e;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < KW; ++k) s = fmaf(ws[co * KW + k], xin[k], s);
+      v[e] = fmaxf(s + bs[co], 0.f);
+    }
+    store16<T>(dst + g * 16, v);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// dispatch
+// ---------------------------------------------------------------------------------
+template <typename T, int WR, int WPX, int TP, int TAPS, int EPI>
+static hipError_t launch_one(const IgemmArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((igemm_kernel<T, WR, WPX, TP, TAPS, EPI>), dim3(a.n_blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, int TAPS, int EPI>
+static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
+  switch (cfg) {
+    case CFG_R128_P128: return launch_one<T, 2, 2, 4, TAPS, EPI>(a, s);
+    case CFG_R64_P128: return launch_one<T, 1, 4, 2, TAPS, EPI>(a, s);
+    case CFG_R64_P256: return launch_one<T, 1, 4, 4, TAPS, EPI>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <typename T>
+static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s) {
+  if (taps == 9) {
+    switch (epi) {
+      case EPI_STORE: return launch_cfg<T, 9, EPI_STORE>(cfg, a, s);
+      case EPI_POOL: return launch_cfg<T, 9, EPI_POOL>(cfg, a, s);
+      case EPI_HEAD:
+        if (cfg == CFG_R128_P128) return hipErrorInvalidValue;
+        return launch_cfg<T, 9, EPI_HEAD>(cfg, a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (taps == 1 && epi == EPI_UPSCATTER) return launch_cfg<T, 1, EPI_UPSCATTER>(cfg, a, s);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s) {
+  switch (t) {
+    case DType::F32: return launch_t<float>(cfg, taps, epi, a, s);
+    case DType::BF16: return launch_t<__bf16>(cfg, taps, epi, a, s);
+    case DType::F16: return launch_t<_Float16>(cfg, taps, epi, a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+static hipError_t first_t(const FirstConvArgs& a, hipStream_t s) {
+  const long long total = (long long)a.N * a.H * a.W;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (a.C == 1) hipLaunchKernelGGL((first_conv_kernel<T, 1>), grid, dim3(256), 0, s, a);
+  else if (a.C == 3) hipLaunchKernelGGL((first_conv_kernel<T, 3>), grid, dim3(256), 0, s, a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s) {
+  switch (t) {
+    case DType::F32: return first_t<float>(a, s);
+    case DType::BF16: return first_t<__bf16>(a, s);
+    case DType::F16: return first_t<_Float16>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+__global__ void nhwc_to_nchw_kernel(const T* __restrict__ src, int N, int H, int W, int C, int ld, int choff,
+                                    float* __restrict__ dst) {
+  const long long total = (long long)N * C * H * W;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int x = (int)(i % W);
+    long long r = i / W;
+    const int y = (int)(r % H);
+    r /= H;
+    const int c = (int)(r % C);
+    const int n = (int)(r / C);
+    dst[i] = (float)src[((long long)(n * H + y) * W + x) * ld + choff + c];
+  }
+}
+
+hipError_t launch_nhwc_to_nchw_f32(DType t, const void* src, int N, int H, int W, int C, int ld,
+                                   int choff, float* dst, hipStream_t s) {
+  const dim3 grid(2048), block(256);
+  switch (t) {
+    case DType::F32:
+      hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, grid, block, 0, s, (const float*)src, N, H, W, C, ld, choff, dst);
+      break;
+    case DType::BF16:
+      hipLaunchKernelGGL(nhwc_to_nchw_kernel<__bf16>, grid, block, 0, s, (const __bf16*)src, N, H, W, C, ld, choff, dst);
+      break;
+    case DType::F16:
+      hipLaunchKernelGGL(nhwc_to_nchw_kernel<_Float16>, grid, block, 0, s, (const _Float16*)src, N, H, W, C, ld, choff, dst);
+      break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace unet

@@ -1,0 +1,104 @@
+"""Drop-in for the reference ``inference.py`` (inference.py:1-129) on the MI355X path.
+
+Same module constants (DEVICE, IMG_SIZE, FIELDS) and functions (load_model,
+preprocess, run_unet) with the same arguments, return values and error classes.
+Differences are internal only:
+  * the model is cached per (checkpoint, mtime, device) instead of re-loaded on every
+    call (the reference re-reads the 124 MB checkpoint per call, inference.py:58);
+  * sigmoid + thresholds run fused in the native head kernel (masks come back as
+    uint8), so the 3x512x512 fp32 probability map never leaves the GPU.
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+import numpy as np
+import torch
+from PIL import Image
+
+from .model import UNet
+
+DEVICE = "cuda" if torch.cuda.is_available() else "cpu"   # inference.py:9
+IMG_SIZE = 512                                            # inference.py:10
+FIELDS = ["invoice_no", "date", "total_amount"]           # inference.py:12
+THRESHOLDS = (0.25, 0.40, 0.30)                           # inference.py:76-78
+CROP_PAD = 0.15                                           # inference.py:106-107
+
+_cache: dict = {}
+_cache_lock = threading.Lock()
+
+
+def load_model(checkpoint_path: str, compute_dtype: str | None = None):
+    """inference.py:17-24: UNet(3,3) on DEVICE, strict state_dict load, eval()."""
+    model = UNet(n_channels=3, n_classes=3, compute_dtype=compute_dtype, thresholds=THRESHOLDS).to(DEVICE)
+    state = torch.load(checkpoint_path, map_location=DEVICE, weights_only=True)
+    model.load_state_dict(state)
+    model.eval()
+    return model
+
+
+def _cached_model(checkpoint_path: str, compute_dtype: str | None = None):
+    key = (os.path.abspath(checkpoint_path), os.path.getmtime(checkpoint_path), DEVICE, compute_dtype)
+    with _cache_lock:
+        m = _cache.get(key)
+        if m is None:
+            m = load_model(checkpoint_path, compute_dtype)
+            _cache.clear()
+            _cache[key] = m
+        return m
+
+
+def preprocess_array(pil_img: Image.Image) -> np.ndarray:
+    """Host half of inference.py:30-44: RGB, resize to 512 (PIL default filter), /255, CHW."""
+    img = pil_img.convert("RGB").resize((IMG_SIZE, IMG_SIZE))
+    arr = np.array(img).astype(np.float32) / 255.0
+    if arr.ndim != 3 or arr.shape[2] != 3:
+        raise ValueError(f"Invalid image shape: {arr.shape}")
+    return arr.transpose(2, 0, 1)
+
+
+def preprocess(pil_img: Image.Image) -> torch.Tensor:
+    """inference.py:30-44: PIL -> Tensor [1, 3, 512, 512] fp32 on DEVICE."""
+    return torch.from_numpy(preprocess_array(pil_img)).unsqueeze(0).to(DEVICE)
+
+
+def masks_to_crops(pil_img: Image.Image, masks: dict) -> dict:
+    """inference.py:84-127: bbox per mask -> original scale -> 15% pad -> crop, rejecting
+    empty / degenerate / near-black crops (None)."""
+    ow, oh = pil_img.size
+    crops = {}
+    for key, mask in masks.items():
+        ys, xs = np.where(mask)
+        if len(xs) == 0 or len(ys) == 0:
+            crops[key] = None
+            continue
+        mx1, mx2 = xs.min(), xs.max()
+        my1, my2 = ys.min(), ys.max()
+        scale_x, scale_y = ow / IMG_SIZE, oh / IMG_SIZE
+        x1, x2 = int(mx1 * scale_x), int(mx2 * scale_x)
+        y1, y2 = int(my1 * scale_y), int(my2 * scale_y)
+        pad_x, pad_y = int((x2 - x1) * CROP_PAD), int((y2 - y1) * CROP_PAD)
+        x1, y1 = max(0, x1 - pad_x), max(0, y1 - pad_y)
+        x2, y2 = min(ow, x2 + pad_x), min(oh, y2 + pad_y)
+        if x2 <= x1 or y2 <= y1:
+            crops[key] = None
+            continue
+        crop = pil_img.crop((x1, y1, x2, y2))
+        arr = np.array(crop)
+        if arr.size == 0 or arr.mean() < 3:
+            crops[key] = None
+            continue
+        crops[key] = crop
+    return crops
+
+
+def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | None = None):
+    """inference.py:50-129 -> (masks: {field: bool[512,512]}, crops: {field: PIL.Image | None})."""
+    model = _cached_model(checkpoint_path, compute_dtype)
+    img_resized = pil_img.resize((IMG_SIZE, IMG_SIZE))            # inference.py:63
+    x = preprocess(img_resized)                                    # inference.py:64
+    with torch.no_grad():
+        m = model.forward_masks(x)[0].cpu().numpy().astype(bool)   # fused sigmoid+threshold
+    masks = {k: m[i] for i, k in enumerate(FIELDS)}
+    return masks, masks_to_crops(pil_img, masks)

@@ -1,0 +1,172 @@
+"""Drop-in ``UNet`` for the reference ``unet_model.UNet`` (unet_model.py:23-86).
+
+Same constructor, same sub-module tree and therefore the same 136 ``state_dict`` keys
+and shapes, so ``load_state_dict(torch.load("checkpoints/best_unet_model.pth"))``
+works unchanged (inference.py:20-21).  ``forward`` runs the MI355X native path
+(libunet_mi355x.so): the parameters held by the torch sub-modules are only the
+weight *container*; they are BN-folded and pre-packed into the native handle the
+first time a forward runs on a device, and again whenever a parameter changes.
+
+There is no CPU / eager fallback: a CPU input raises.
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+import torch
+import torch.nn as nn
+
+from . import native
+
+DEFAULT_DTYPE = os.environ.get("UNET_MI355X_DTYPE", "fp32")
+
+
+class DoubleConv(nn.Module):
+    """Parameter container matching unet_model.py:6-17 (conv3x3, BN, ReLU) x 2.
+
+    The native path executes DoubleConv blocks only inside the whole-network
+    forward (fused with pooling / concat / head), so calling a block on its own is
+    not supported.
+    """
+
+    def __init__(self, in_ch: int, out_ch: int):
+        super().__init__()
+        self.net = nn.Sequential(
+            nn.Conv2d(in_ch, out_ch, kernel_size=3, padding=1),
+            nn.BatchNorm2d(out_ch),
+            nn.ReLU(inplace=True),
+            nn.Conv2d(out_ch, out_ch, kernel_size=3, padding=1),
+            nn.BatchNorm2d(out_ch),
+            nn.ReLU(inplace=True),
+        )
+
+    def forward(self, x):  # pragma: no cover - documented limitation
+        raise RuntimeError("unet_mi355x: DoubleConv runs only inside UNet.forward (fused native path)")
+
+
+class UNet(nn.Module):
+    """unet_model.UNet(n_channels=3, n_classes=3) with an MI355X forward.
+
+    compute_dtype: "fp32" (default; exact fp32 MFMA, reference semantics), "bf16" or
+    "fp16" (16-bit activations/weights, fp32 accumulation, fp32 head).  Default from
+    the UNET_MI355X_DTYPE environment variable.
+    """
+
+    def __init__(self, n_channels: int = 3, n_classes: int = 3, compute_dtype: str | None = None,
+                 thresholds=(0.25, 0.40, 0.30)):
+        super().__init__()
+        self.n_channels = n_channels
+        self.n_classes = n_classes
+        self.compute_dtype = compute_dtype or DEFAULT_DTYPE
+        if self.compute_dtype not in native.DTYPES:
+            raise ValueError(f"compute_dtype must be one of {sorted(native.DTYPES)}")
+        self.thresholds = tuple(float(t) for t in thresholds)
+
+        self.down1 = DoubleConv(n_channels, 64)
+        self.down2 = DoubleConv(64, 128)
+        self.down3 = DoubleConv(128, 256)
+        self.down4 = DoubleConv(256, 512)
+        self.pool = nn.MaxPool2d(2)
+        self.bottleneck = DoubleConv(512, 1024)
+        self.up4 = nn.ConvTranspose2d(1024, 512, 2, stride=2)
+        self.conv4 = DoubleConv(1024, 512)
+        self.up3 = nn.ConvTranspose2d(512, 256, 2, stride=2)
+        self.conv3 = DoubleConv(512, 256)
+        self.up2 = nn.ConvTranspose2d(256, 128, 2, stride=2)
+        self.conv2 = DoubleConv(256, 128)
+        self.up1 = nn.ConvTranspose2d(128, 64, 2, stride=2)
+        self.conv1 = DoubleConv(128, 64)
+        self.out_conv = nn.Conv2d(64, n_classes, kernel_size=1)
+        nn.init.constant_(self.out_conv.bias, -4)  # unet_model.py:52-53
+
+        self._handles: dict[int, native.Handle] = {}
+        self._packed_sig: dict[int, tuple] = {}
+        self._lock = threading.Lock()
+
+    # ------------------------------------------------------------------ native plumbing
+    def _signature(self):
+        return tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
+
+    def native_handle(self, device: torch.device) -> native.Handle:
+        """The packed native handle for ``device`` (re-packs if any parameter changed)."""
+        if device.type != "cuda":
+            raise RuntimeError("unet_mi355x: UNet.forward runs only on a ROCm GPU tensor "
+                               f"(got device {device}); there is no CPU fallback")
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        with self._lock:
+            h = self._handles.get(idx)
+            if h is None:
+                h = native.Handle(self.n_channels, self.n_classes, self.compute_dtype, idx,
+                                  self.thresholds)
+                self._handles[idx] = h
+            sig = self._signature()
+            if self._packed_sig.get(idx) != sig:
+                h.load_weights(self.state_dict())
+                self._packed_sig[idx] = sig
+        return h
+
+    def _check_input(self, x: torch.Tensor):
+        if not isinstance(x, torch.Tensor) or x.dim() != 4:
+            raise RuntimeError("UNet.forward expects a 4-D NCHW tensor")
+        if x.shape[1] != self.n_channels:
+            raise RuntimeError(f"expected input with {self.n_channels} channels, got {x.shape[1]}")
+        if x.shape[2] % 16 or x.shape[3] % 16:
+            # the reference fails inside torch.cat for such sizes
+            raise RuntimeError(f"UNet input H and W must be divisible by 16, got {tuple(x.shape[2:])}")
+
+    def _run(self, x: torch.Tensor, want_logits: bool, mask_kind: int):
+        self._check_input(x)
+        h = self.native_handle(x.device)
+        x = x.detach()
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.to(torch.float32).contiguous()
+        n, _, hh, ww = x.shape
+        logits = masks = None
+        if want_logits:
+            logits = torch.empty((n, self.n_classes, hh, ww), device=x.device, dtype=torch.float32)
+        if mask_kind == native.MASK_U8:
+            masks = torch.empty((n, self.n_classes, hh, ww), device=x.device, dtype=torch.uint8)
+        elif mask_kind == native.MASK_BITS:
+            masks = torch.empty((n, self.n_classes, hh, ww // 8), device=x.device, dtype=torch.uint8)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        with torch.cuda.device(x.device):
+            h.forward(x, logits, masks, mask_kind, stream)
+        return logits, masks
+
+    # ------------------------------------------------------------------ public API
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """unet_model.py:55-86: NCHW fp32 in -> NCHW fp32 logits [N, n_classes, H, W]."""
+        logits, _ = self._run(x, True, native.MASK_NONE)
+        return logits
+
+    def forward_masks(self, x: torch.Tensor, packed: bool = False, with_logits: bool = False):
+        """Fused sigmoid + per-class threshold (inference.py:72-79) on the device.
+
+        Returns uint8 masks [N, n_classes, H, W] (0/1), or bit-packed [N, n_classes, H, W/8]
+        (bit b of byte j = pixel 8j+b) when ``packed``; with ``with_logits`` also the logits.
+        """
+        logits, masks = self._run(x, with_logits, native.MASK_BITS if packed else native.MASK_U8)
+        return (masks, logits) if with_logits else masks
+
+    def reserve(self, n: int, h: int, w: int, device=None) -> None:
+        """Pre-allocate the native workspace (so forwards do not allocate)."""
+        dev = torch.device(device) if device is not None else next(self.parameters()).device
+        self.native_handle(dev).reserve(n, h, w)
+
+    def intermediate(self, name: str, device=None) -> torch.Tensor:
+        """Intermediate activation of the last forward as fp32 NCHW (debug / per-layer parity)."""
+        dev = torch.device(device) if device is not None else next(self.parameters()).device
+        h = self.native_handle(dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        numel = h.debug_fetch(name, stream)
+        out = torch.empty(numel, device=dev, dtype=torch.float32)
+        with torch.cuda.device(dev):
+            h.debug_fetch_into(name, out, stream)
+        return out
+
+    def close(self):
+        for h in self._handles.values():
+            h.close()
+        self._handles.clear()
+        self._packed_sig.clear()

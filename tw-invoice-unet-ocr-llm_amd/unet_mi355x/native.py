@@ -1,0 +1,172 @@
+"""ctypes binding of libunet_mi355x.so (the C-ABI declared in include/unet_mi355x.h).
+
+torch is imported first on purpose: the library's NEEDED ``libamdhip64.so.7`` then
+resolves to the HIP runtime torch already loaded, so torch device pointers and
+``torch.cuda`` streams are valid inside the library.  There is no fallback: if the
+library is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+import torch  # noqa: F401  (must precede the library load, see module docstring)
+
+LIB_NAME = "libunet_mi355x.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+UNET_OK, UNET_EINVAL, UNET_ESHAPE, UNET_ENOMEM, UNET_EHIP, UNET_ESTATE, UNET_EKEY = 0, -1, -2, -3, -4, -5, -6
+DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16": 2}
+MASK_NONE, MASK_U8, MASK_BITS = 0, 1, 2
+LAYOUT_NCHW, IN_F32 = 0, 0
+
+# every function include/unet_mi355x.h declares: name -> (restype, argtypes)
+_vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+
+
+class UnetConfig(ctypes.Structure):
+    _fields_ = [("n_channels", ctypes.c_int), ("n_classes", ctypes.c_int), ("dtype", ctypes.c_int),
+                ("device", ctypes.c_int), ("thresholds", ctypes.c_float * 4)]
+
+
+class TensorView(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.c_void_p), ("dtype", ctypes.c_int),
+                ("ndim", ctypes.c_int), ("shape", ctypes.c_int64 * 4)]
+
+
+SIGNATURES = {
+    "unet_create": (_i, [ctypes.POINTER(UnetConfig), ctypes.POINTER(_vp)]),
+    "unet_load_weights": (_i, [_vp, ctypes.POINTER(TensorView), _i]),
+    "unet_workspace_bytes": (_sz, [_vp, _i, _i, _i]),
+    "unet_reserve": (_i, [_vp, _i, _i, _i]),
+    "unet_forward": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp]),
+    "unet_num_launches": (_i, []),
+    "unet_forward_timed": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
+    "unet_debug_fetch": (_i, [_vp, ctypes.c_char_p, _vp, ctypes.POINTER(_sz), _vp]),
+    "unet_destroy": (_i, [_vp]),
+    "unet_last_error": (ctypes.c_char_p, []),
+    "unet_abi_version": (_i, []),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH):
+    """Load (once) and type the native library; raises RuntimeError if it is absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"unet_mi355x: native library {path} not built; run "
+                "`make -C tw-invoice-unet-ocr-llm_amd/csrc` (or __graft_entry__.build()). "
+                "There is no CPU/PyTorch fallback.")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.unet_abi_version() != 1:
+            raise RuntimeError("unet_mi355x: ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc == UNET_OK:
+        return
+    msg = f"{what}: {load_library().unet_last_error().decode(errors='replace')}"
+    if rc == UNET_EINVAL:
+        raise ValueError(msg)
+    if rc == UNET_ENOMEM:
+        raise torch.cuda.OutOfMemoryError(msg) if hasattr(torch.cuda, "OutOfMemoryError") else MemoryError(msg)
+    raise RuntimeError(msg)
+
+
+class Handle:
+    """One native handle = one device, one packed weight set, one workspace (not re-entrant)."""
+
+    def __init__(self, n_channels: int, n_classes: int, dtype: str, device: int,
+                 thresholds=(0.25, 0.40, 0.30, 0.5)):
+        self.lib = load_library()
+        self.n_channels, self.n_classes, self.device = n_channels, n_classes, device
+        self.dtype = dtype
+        cfg = UnetConfig(n_channels, n_classes, DTYPES[dtype], device,
+                         (ctypes.c_float * 4)(*[float(t) for t in list(thresholds)[:4]] +
+                                              [0.5] * (4 - len(list(thresholds)[:4]))))
+        h = ctypes.c_void_p()
+        check(self.lib.unet_create(ctypes.byref(cfg), ctypes.byref(h)), "unet_create")
+        self._h = h
+        self.lock = threading.Lock()
+
+    def load_weights(self, state_dict) -> None:
+        """state_dict: mapping name -> torch.Tensor / np.ndarray (any device); strict."""
+        keep, views = [], []
+        for k, v in state_dict.items():
+            arr = v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v)
+            if arr.dtype.kind == "f":
+                arr = np.ascontiguousarray(arr, dtype=np.float32)
+                code = 0
+            else:
+                arr = np.ascontiguousarray(arr, dtype=np.int64)
+                code = 1
+            keep.append(arr)
+            shape = list(arr.shape) + [0] * (4 - arr.ndim)
+            views.append(TensorView(k.encode(), arr.ctypes.data, code, arr.ndim, (ctypes.c_int64 * 4)(*shape)))
+        arr_t = (TensorView * len(views))(*views)
+        with self.lock:
+            check(self.lib.unet_load_weights(self._h, arr_t, len(views)), "unet_load_weights")
+
+    def workspace_bytes(self, n: int, h: int, w: int) -> int:
+        return int(self.lib.unet_workspace_bytes(self._h, n, h, w))
+
+    def reserve(self, n: int, h: int, w: int) -> None:
+        with self.lock:
+            check(self.lib.unet_reserve(self._h, n, h, w), "unet_reserve")
+
+    def forward(self, x: torch.Tensor, logits: torch.Tensor | None, masks: torch.Tensor | None,
+                mask_kind: int, stream: int) -> None:
+        n, c, h, w = x.shape
+        with self.lock:
+            check(self.lib.unet_forward(self._h, x.data_ptr(), LAYOUT_NCHW, IN_F32,
+                                        None if logits is None else logits.data_ptr(),
+                                        None if masks is None else masks.data_ptr(),
+                                        mask_kind, n, h, w, stream), "unet_forward")
+
+    def forward_timed(self, x: torch.Tensor, logits: torch.Tensor | None, masks: torch.Tensor | None,
+                      mask_kind: int, stream: int) -> list:
+        """forward + HIP-event time (ms) of every launch, in include/unet_mi355x.h order."""
+        n, c, h, w = x.shape
+        nl = self.lib.unet_num_launches()
+        ms = (ctypes.c_float * nl)()
+        with self.lock:
+            check(self.lib.unet_forward_timed(self._h, x.data_ptr(), LAYOUT_NCHW, IN_F32,
+                                              None if logits is None else logits.data_ptr(),
+                                              None if masks is None else masks.data_ptr(),
+                                              mask_kind, n, h, w, stream, ms), "unet_forward_timed")
+        return list(ms)
+
+    def debug_fetch(self, name: str, stream: int) -> int:
+        cnt = ctypes.c_size_t(0)
+        check(self.lib.unet_debug_fetch(self._h, name.encode(), None, ctypes.byref(cnt), stream), "unet_debug_fetch")
+        return int(cnt.value)
+
+    def debug_fetch_into(self, name: str, dst: torch.Tensor, stream: int) -> None:
+        cnt = ctypes.c_size_t(0)
+        check(self.lib.unet_debug_fetch(self._h, name.encode(), dst.data_ptr(), ctypes.byref(cnt), stream),
+              "unet_debug_fetch")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.unet_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
