@@ -1,0 +1,237 @@
+#!/usr/bin/env python
+"""bench.py -- invoice masks/sec of the MI355X UNet forward path (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch of synthetic invoice pages resident in
+HBM: UNet(3,3) forward at 512x512 (unet_model.py:55-86) with the fused sigmoid +
+per-field threshold (inference.py:72-79) producing bit-packed masks, plus -- for N>1 --
+the RCCL all-gather of the masks over xGMI.  Per-GPU batch is fixed (weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--dtype bf16]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (the driver does this for N>1)
+
+Rank 0 prints ONE JSON line.  Extra fields: roofline (dominant kernel, HIP-event timed
+inside this run), cpu_baseline (the oracle on this host's cores, bounded sample, with
+mask IoU of the GPU masks against it), kernels (per-instantiation time breakdown).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "tw-invoice-unet-ocr-llm_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from unet_mi355x import native  # noqa: E402
+from unet_mi355x import synthetic as syn  # noqa: E402
+from unet_mi355x.model import UNet  # noqa: E402
+
+METRIC = "invoice masks/sec at 512x512 bs256, 1/2/4/8 MI355X; IoU vs CPU ref"
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+# launch order of include/unet_mi355x.h: (name, kernel instantiation, cin, cout, level, kind)
+LAUNCHES = [
+    ("down1.0", "first_conv", None, 64, 0, "first"),
+    ("down1.3", "igemm_r64p256_pool", 64, 64, 0, "c3"),
+    ("down2.0", "igemm_r128p128_store", 64, 128, 1, "c3"),
+    ("down2.3", "igemm_r128p128_pool", 128, 128, 1, "c3"),
+    ("down3.0", "igemm_r128p128_store", 128, 256, 2, "c3"),
+    ("down3.3", "igemm_r128p128_pool", 256, 256, 2, "c3"),
+    ("down4.0", "igemm_r128p128_store", 256, 512, 3, "c3"),
+    ("down4.3", "igemm_r128p128_pool", 512, 512, 3, "c3"),
+    ("bottleneck.0", "igemm_r128p128_store", 512, 1024, 4, "c3"),
+    ("bottleneck.3", "igemm_r128p128_store", 1024, 1024, 4, "c3"),
+    ("up4", "igemm_r128p128_upscatter", 1024, 512, 4, "up"),
+    ("conv4.0", "igemm_r128p128_store", 1024, 512, 3, "c3"),
+    ("conv4.3", "igemm_r128p128_store", 512, 512, 3, "c3"),
+    ("up3", "igemm_r128p128_upscatter", 512, 256, 3, "up"),
+    ("conv3.0", "igemm_r128p128_store", 512, 256, 2, "c3"),
+    ("conv3.3", "igemm_r128p128_store", 256, 256, 2, "c3"),
+    ("up2", "igemm_r128p128_upscatter", 256, 128, 2, "up"),
+    ("conv2.0", "igemm_r128p128_store", 256, 128, 1, "c3"),
+    ("conv2.3", "igemm_r128p128_store", 128, 128, 1, "c3"),
+    ("up1", "igemm_r128p128_upscatter", 128, 64, 1, "up"),
+    ("conv1.0", "igemm_r64p256_store", 128, 64, 0, "c3"),
+    ("conv1.3", "igemm_r64p128_head", 64, 64, 0, "c3"),
+]
+KERNEL_SYMBOL = {  # template arguments <T, WR, WPX, TP, TAPS, EPI> of unet::igemm_kernel
+    "igemm_r128p128_store": "2, 2, 4, 9, 0", "igemm_r128p128_pool": "2, 2, 4, 9, 1",
+    "igemm_r128p128_upscatter": "2, 2, 4, 1, 3", "igemm_r64p256_pool": "1, 4, 4, 9, 1",
+    "igemm_r64p256_store": "1, 4, 4, 9, 0", "igemm_r64p128_head": "1, 4, 2, 9, 2",
+}
+
+
+def launch_flops(entry, n, h, w, c_in, ncls=3):
+    """Algorithmic FLOPs (2 per MAC) of one launch over n images of h x w."""
+    name, _, cin, cout, lvl, kind = entry
+    hh, ww = h >> lvl, w >> lvl
+    if kind == "first":
+        return 2.0 * 9 * c_in * cout * hh * ww * n
+    if kind == "up":   # input at level lvl, output at lvl-1: every input pixel -> 4 outputs
+        return 2.0 * cin * 4 * cout * hh * ww * n
+    f = 2.0 * 9 * cin * cout * hh * ww * n
+    if name == "conv1.3":
+        f += 2.0 * 64 * ncls * hh * ww * n     # fused 1x1 out_conv
+    return f
+
+
+def gen_pages(seed, batch, size, channels, unique=32):
+    """Synthetic invoice pages; `unique` distinct pages tiled to the batch (generation cost)."""
+    u = min(unique, batch)
+    pages = syn.invoice_pages(seed, u, size, size, channels)
+    reps = (batch + u - 1) // u
+    return np.ascontiguousarray(np.concatenate([pages] * reps, axis=0)[:batch])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--channels", type=int, default=3)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-layer-profile", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary (profiles/*.json) to fill roofline.traffic")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B, S, C = args.batch, args.size, args.channels
+    # weights: structured synthetic (the real checkpoint is an LFS pointer); out_conv bias
+    # re-centred below so that masks are non-trivial (~10% of each field's pixels).
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in syn.make_state_dict(0, C, 3, "structured").items()}
+    model = UNet(C, 3, compute_dtype=args.dtype)
+    model.load_state_dict(sd)
+    model = model.to(dev).eval()
+    x = torch.from_numpy(gen_pages(1000 + rank, B, S, C)).to(dev)
+    with torch.no_grad():
+        lg = model(x[:2])
+    thr = torch.tensor([0.25, 0.40, 0.30], dtype=torch.float64)
+    q = torch.quantile(lg.double().transpose(0, 1).reshape(3, -1).cpu(), 0.9, dim=1)
+    shift = (torch.log(thr / (1 - thr)) - q).float()
+    if world > 1:   # identical weights on every rank
+        shift = shift.to(dev)
+        dist.broadcast(shift, 0)
+        shift = shift.cpu()
+    with torch.no_grad():
+        model.out_conv.bias.add_(shift.to(dev))
+    handle = model.native_handle(dev)
+    handle.reserve(B, S, S)
+
+    masks = torch.empty((B, 3, S, S // 8), dtype=torch.uint8, device=dev)
+    gathered = torch.empty((world * B, 3, S, S // 8), dtype=torch.uint8, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        handle.forward(x, None, masks, native.MASK_BITS, stream)
+        if gathered is not None:
+            dist.all_gather_into_tensor(gathered, masks)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = world * B * args.steps / elapsed
+
+    # ---- per-launch HIP-event timing (same stream) -> dominant kernel roofline
+    kernels, roofline = {}, None
+    if not args.no_layer_profile:
+        ms = handle.forward_timed(x, None, masks, native.MASK_BITS, stream)
+        for entry, t in zip(LAUNCHES, ms):
+            k = kernels.setdefault(entry[1], {"launches": 0, "ms": 0.0, "gflop": 0.0})
+            k["launches"] += 1
+            k["ms"] += t
+            k["gflop"] += launch_flops(entry, B, S, S, C) / 1e9
+        for k in kernels.values():
+            k["tflops"] = round(k["gflop"] / k["ms"], 1) if k["ms"] > 0 else None
+            k["ms"] = round(k["ms"], 3)
+            k["gflop"] = round(k["gflop"], 1)
+        dom_name, dom = max(((n, k) for n, k in kernels.items() if n.startswith("igemm")), key=lambda kv: kv[1]["ms"])
+        achieved = dom["gflop"] / dom["ms"]   # TFLOP/s (GFLOP / ms)
+        peak = PEAK_TFLOPS[args.dtype]
+        traffic = None
+        if args.traffic_json and os.path.exists(args.traffic_json):
+            tj = json.load(open(args.traffic_json))
+            traffic = tj.get(dom_name, {}).get("hbm_bytes_per_launch")
+        roofline = {"bound": "mfma", "kernel": dom_name,
+                    "symbol": f"unet::igemm_kernel<{ {'bf16': '__bf16', 'fp16': '_Float16', 'fp32': 'float'}[args.dtype]}, {KERNEL_SYMBOL[dom_name]}>",
+                    "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 4), "traffic": traffic,
+                    "launches_per_step": dom["launches"],
+                    "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
+                    "whole_step_tflops": round(sum(launch_flops(e, B, S, S, C) for e in LAUNCHES) / 1e9 /
+                                               sum(ms), 1)}
+
+    # ---- CPU baseline (the oracle, fp32 eager on this host), rank 0 at N=1 only
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import unet_oracle as orc
+        sd_cpu = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        nthreads = torch.get_num_threads()
+        xc = x[:64].cpu()
+        mk = np.unpackbits(masks[:64].cpu().numpy(), axis=-1, bitorder="little").astype(bool)
+        orc.unet_forward(sd_cpu, xc[:1, :, :64, :64])  # warm the CPU kernels
+        done, ious, t0 = 0, [], time.perf_counter()
+        while done < xc.shape[0] and (done == 0 or time.perf_counter() - t0 < args.cpu_seconds):
+            lg = orc.unet_forward(sd_cpu, xc[done:done + 1]).numpy()[0]
+            ref = orc.masks_from_logits(lg)
+            ious += [orc.mask_iou(mk[done, i], ref[f]) for i, f in enumerate(orc.FIELDS)]
+            done += 1
+        t_cpu = time.perf_counter() - t0
+        cpu = {"value": round(done / t_cpu, 4), "unit": "images/s", "cores": nthreads, "kind": "port",
+               "sample": f"{done} of the bench images, batch 1, {S}x{S}, fp32 eager torch (oracle/unet_oracle.py)",
+               "iou_vs_cpu": {"min": round(min(ious), 5), "mean": round(float(np.mean(ious)), 5),
+                              "images": done, "gpu_dtype": args.dtype}}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (seeded invoice-like pages, gray x3; structured random weights -- "
+                    "the trained checkpoint is an LFS pointer)",
+            "config": {"workload": f"UNet(n_channels={C}, n_classes=3) forward {S}x{S} + fused sigmoid/"
+                                   f"threshold bit-packed masks" + (" + RCCL all-gather" if world > 1 else ""),
+                       "global_batch": world * B, "per_gpu_batch": B, "image": S,
+                       "parallelism": f"dp{world}"},
+            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

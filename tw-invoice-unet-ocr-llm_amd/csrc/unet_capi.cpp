@@ -8,6 +8,7 @@
 #include "../../include/unet_mi355x.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -265,13 +266,47 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   unet_handle* h = new unet_handle();
   h->cfg = *cfg;
   h->dt = (DType)cfg->dtype;
+  // Kernel configuration per layer (tuned on MI355X).  Overrides for
+  // tuning / A-B runs: UNET_MI355X_PRESET=gather (first-generation per-tap kernel for
+  // every layer) and UNET_MI355X_CFG="layer:cfg,..." (layer = index into L[], cfg = Cfg).
+  const char* preset = std::getenv("UNET_MI355X_PRESET");
+  const std::string ps = preset ? preset : "";
+  const int chunk = cfg->dtype == UNET_DTYPE_F32 ? 32 : 64;   // channels per 128-byte chunk
   for (int i = 0; i < 17; ++i) {
-    h->L[i].cin = kLayerCh[i][0];
-    h->L[i].cout = h->L[i].ctot = kLayerCh[i][1];
-    h->L[i].taps = 9;
-    h->L[i].cfg = h->L[i].cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
+    Layer& L = h->L[i];
+    L.cin = kLayerCh[i][0];
+    L.cout = L.ctot = kLayerCh[i][1];
+    L.taps = 9;
+    if (ps == "gather") {
+      L.cfg = L.cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
+    } else if (L.cout == 64) {
+      L.cfg = L.cin == chunk ? CFG_HALO1_R64_W8 : CFG_R64_P256;
+    } else {
+      L.cfg = CFG_HALO_R128_W8;
+    }
   }
-  h->L[C1B].cfg = CFG_R64_P128;
+  if (ps == "gather") h->L[C1B].cfg = CFG_R64_P128;
+  if (const char* ov = std::getenv("UNET_MI355X_CFG")) {
+    std::string o(ov);
+    size_t pos = 0;
+    while (pos < o.size()) {
+      size_t end = o.find(',', pos);
+      if (end == std::string::npos) end = o.size();
+      const std::string item = o.substr(pos, end - pos);
+      const size_t colon = item.find(':');
+      if (colon != std::string::npos) {
+        const int li = std::atoi(item.substr(0, colon).c_str()), c = std::atoi(item.substr(colon + 1).c_str());
+        if (li >= 0 && li < 17 && c >= 0 && c < CFG_COUNT) h->L[li].cfg = c;
+      }
+      pos = end + 1;
+    }
+  }
+  for (int i = 0; i < 17; ++i) {   // keep every layer on a configuration it supports
+    Layer& L = h->L[i];
+    if (cfg_rows(L.cfg) > L.cout || (cfg_single_chunk(L.cfg) && L.cin != chunk))
+      L.cfg = L.cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
+    if (i == C1B && cfg_rows(L.cfg) != 64) L.cfg = CFG_R64_P128;
+  }
   for (int i = 0; i < 4; ++i) {
     h->U[i].cin = kUpCh[i][0];
     h->U[i].cout = kUpCh[i][1];

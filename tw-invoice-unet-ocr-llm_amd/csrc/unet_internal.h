@@ -57,9 +57,18 @@ struct FirstConvArgs {
 };
 
 // Kernel configurations (rows tile x pixel tile).
-enum Cfg : int { CFG_R128_P128 = 0, CFG_R64_P128 = 1, CFG_R64_P256 = 2, CFG_R128_P256 = 3 };
+// CFG_R*_P*: per-tap gathered B tile (rows x pixels, tile 16 px wide); CFG_HALO_*: 16x16
+// pixel tile with an LDS halo (3x3 only), R = rows per block, W = waves per block.
+enum Cfg : int {
+  CFG_R128_P128 = 0, CFG_R64_P128 = 1, CFG_R64_P256 = 2, CFG_R128_P256 = 3,
+  CFG_HALO_R128_W4 = 4, CFG_HALO_R128_W8 = 5, CFG_HALO_R64_W4 = 6, CFG_HALO_R64_W8 = 7,
+  CFG_HALO1_R64_W4 = 8, CFG_HALO1_R64_W8 = 9,   // single halo buffer, Cin == one 128-B chunk
+  CFG_COUNT = 10
+};
+bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);
 int cfg_pixels(int cfg);
+bool cfg_is_halo(int cfg);
 
 hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s);
 hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s);

@@ -28,8 +28,12 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-int cfg_rows(int cfg) { return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256) ? 128 : 64; }
-int cfg_pixels(int cfg) { return (cfg == CFG_R64_P256 || cfg == CFG_R128_P256) ? 256 : 128; }
+int cfg_rows(int cfg) {
+  return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8) ? 128 : 64;
+}
+bool cfg_single_chunk(int cfg) { return cfg == CFG_HALO1_R64_W4 || cfg == CFG_HALO1_R64_W8; }
+int cfg_pixels(int cfg) { return (cfg == CFG_R64_P128 || cfg == CFG_R128_P128) ? 128 : 256; }
+bool cfg_is_halo(int cfg) { return cfg >= CFG_HALO_R128_W4; }
 
 // ---------------------------------------------------------------------------------
 // element traits
@@ -93,8 +97,24 @@ __device__ __forceinline__ void store16<_Float16>(_Float16* dst, const float (&v
   d[1] = __builtin_bit_cast(uint4, hi);
 }
 
+// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4): lane l's bytes land at
+// lds_dst + 16*l.  Issued from inline asm on purpose: hipcc would otherwise treat every
+// later ds_read as aliasing the in-flight DMA and drain vmcnt(0) in front of it, which
+// serialises the load of step s+2 behind the compute of step s.  The waits are ours
+// (counted vmcnt before each barrier); M0 is saved/restored inside the statement.
 __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
-  __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_dst, 16, 0, 0);
+  const uint32_t lds_addr = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_t)lds_dst)));
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_addr)
+      : "memory");
 }
 
 // Pixel p (0..BP-1) of a block tile -> (row, col) inside the TH x 16 tile.  Pixels come
@@ -105,6 +125,105 @@ __device__ __forceinline__ void pix_of(int p, int& py, int& px) {
   py = 2 * (g >> 1) + (j >> 3);
   px = 8 * (g & 1) + (j & 7);
 }
+
+// ---------------------------------------------------------------------------------
+// shared epilogue
+// ---------------------------------------------------------------------------------
+// Lane holds, for pixel column (lane & 15) of each p tile, the 16 consecutive natural
+// rows rbase .. rbase+15 (the weight packing permutes rows so that MFMA row
+// 4*(lane>>4)+e of row-tile t is natural row 16*(lane>>4) + 4*t + e).
+// Pixel p of the wave = group (g0 + p) of the block tile whose origin is (oy0, ox0).
+template <typename T, int TP, int EPI>
+__device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0,
+                                              int ox0, int g0, int row0, const float* bias_w,
+                                              const float* head_w, const float* head_b) {
+  // bias_w: bias of this wave's 64 rows (global or LDS); head_w: [ncls][64] with the
+  // wave's 64 rows at +0 (EPI_HEAD only, single 64-row tile); head_b: [ncls]
+  constexpr int TC = 4;
+  const int H = a.H, W = a.W;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4;
+  const int col = lane & 15;
+  const int rbase = row0 + q * 16;
+  float bv[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias_w + q * 16 + 4 * i);
+    bv[4 * i] = b4[0]; bv[4 * i + 1] = b4[1]; bv[4 * i + 2] = b4[2]; bv[4 * i + 3] = b4[3];
+  }
+
+#pragma unroll
+  for (int p = 0; p < TP; ++p) {
+    int py, px;
+    pix_of((g0 + p) * 16 + col, py, px);
+    const int oy = oy0 + py, ox = ox0 + px;
+    const bool inside = oy < H && ox < W;
+    float v[16];
+#pragma unroll
+    for (int t = 0; t < TC; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = acc[t][p][e] + bv[t * 4 + e];
+        if (EPI != EPI_UPSCATTER) x = fmaxf(x, 0.f);
+        v[t * 4 + e] = x;
+      }
+    if constexpr (EPI == EPI_STORE || EPI == EPI_POOL) {
+      if (inside) {
+        T* dst = reinterpret_cast<T*>(a.out) + ((long long)(n * H + oy) * W + ox) * a.ldo + a.out_off + rbase;
+        store16<T>(dst, v);
+      }
+      if constexpr (EPI == EPI_POOL) {
+        float m[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          float o = fmaxf(v[e], __shfl_xor(v[e], 1));
+          m[e] = fmaxf(o, __shfl_xor(o, 8));
+        }
+        if ((col & 9) == 0 && oy + 1 < H && ox + 1 < W) {
+          const int Ho = H >> 1, Wo = W >> 1;
+          T* dst = reinterpret_cast<T*>(a.out2) +
+                   ((long long)(n * Ho + (oy >> 1)) * Wo + (ox >> 1)) * a.ldo2 + rbase;
+          store16<T>(dst, m);
+        }
+      }
+    } else if constexpr (EPI == EPI_UPSCATTER) {
+      if (inside) {
+        const int ab = rbase / a.Cout;
+        const int o0 = rbase - ab * a.Cout;
+        const int Y = 2 * oy + (ab >> 1), X = 2 * ox + (ab & 1);
+        T* dst = reinterpret_cast<T*>(a.out) +
+                 ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0;
+        store16<T>(dst, v);
+      }
+    } else {  // EPI_HEAD: 1x1 conv 64 -> ncls on the fp32 activations, then masks
+      for (int c = 0; c < a.ncls; ++c) {
+        const float* hw = head_w + c * 64 + q * 16;
+        float sum = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sum = fmaf(hw[e], v[e], sum);
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+        const float logit = sum + head_b[c];
+        const long long pix = ((long long)(n * a.ncls + c) * H + oy) * W + ox;
+        if (a.logits && q == 0 && inside) a.logits[pix] = logit;
+        if (a.mask_kind != MASK_NONE) {
+          const float prob = 1.0f / (1.0f + expf(-logit));   // torch.sigmoid, inference.py:72
+          const bool on = prob > a.thr[c];                    // strict '>', inference.py:76-78
+          if (a.mask_kind == MASK_U8) {
+            if (q == 0 && inside) a.masks[pix] = on ? 1 : 0;
+          } else {
+            const unsigned long long bal = __ballot(on);
+            if (q == 0 && (col & 7) == 0 && inside) {
+              const unsigned byte = (unsigned)(bal >> (col & 8)) & 0xFFu;
+              a.masks[((long long)(n * a.ncls + c) * H + oy) * (W >> 3) + (ox >> 3)] = (uint8_t)byte;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
 
 // ---------------------------------------------------------------------------------
 // implicit-GEMM kernel
@@ -229,88 +348,215 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IgemmArgs a) {
     __syncthreads();
   }
 
-  // ---------------------------------------------------------------- epilogue
-  // Lane holds, for pixel column (lane & 15) of each p tile, the 16 consecutive natural
-  // rows rbase .. rbase+15 (the weight packing permutes rows so that MFMA row
-  // 4*(lane>>4)+e of row-tile t is natural row 16*(lane>>4) + 4*t + e).
-  const int q = lane >> 4;
-  const int col = lane & 15;
-  const int rbase = ct * BR + wr * 64 + q * 16;
-  float bv[16];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + rbase + 4 * i);
-    bv[4 * i] = b4[0]; bv[4 * i + 1] = b4[1]; bv[4 * i + 2] = b4[2]; bv[4 * i + 3] = b4[3];
-  }
+  conv_epilogue<T, TP, EPI>(a, acc, n, ty * TH, tx * 16, wp * TP, ct * BR + wr * 64,
+                            a.bias + ct * BR + wr * 64, a.head_w + wr * 64, a.head_b);
+}
 
+// ---------------------------------------------------------------------------------
+// 3x3 conv with an LDS halo tile (the main kernel for 3x3 layers)
+// ---------------------------------------------------------------------------------
+// Block = BR output channels x a 16x16 output-pixel tile.  Per 64-channel (128-byte) input
+// chunk the block stages the 18x18 input halo ONCE into LDS; the nine taps then read
+// shifted windows of it, so the activation operand is fetched from L2 once per chunk
+// instead of nine times.  Weights stream through a 3-slot ring, two K-steps ahead.  All
+// staging is LDS-DMA (global_load_lds_dwordx4) with counted vmcnt waits, so loads stay in
+// flight across the per-step barrier.
+//
+// LDS: [halo 0][halo 1][w slot 0][w slot 1][w slot 2]; halo pixel (hy,hx) -> row hy*18+hx
+// (128 B), 16-byte chunk c stored at c ^ (hx & 7): conflict-free ds_read_b128 for every tap
+// (the 18-pixel row stride breaks the usual row&7 swizzle).  Weight rows: c ^ (row & 7).
+constexpr int kHaloPix = 18 * 18;
+constexpr int kPersistBlocks = 256;   // one resident block per CU (LDS-limited)
+
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+template <typename T, int WR, int WPX, int HB, int EPI>
+__global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void conv3x3_halo_kernel(const IgemmArgs a) {
+  // HB = 2 (persistent): gridDim.x = n_ct * n_slots blocks (host), each with a fixed row
+  // tile ct, walks pixel tiles mt = slot, slot + n_slots, ...  The K-step pipeline (halo of
+  // the next chunk, weights two steps ahead) runs continuously across tile boundaries, so
+  // the next tile's loads overlap this tile's last steps and epilogue.
+  // HB = 1: one halo buffer, one tile per block, a single 64-channel chunk (Cin = BKE):
+  // small enough for two blocks per CU, which then overlap each other's epilogue.
+  constexpr int NW = WR * WPX;
+  constexpr int TC = 4;
+  constexpr int TP = 16 / WPX;
+  constexpr int BR = WR * 64;
+  constexpr int BKE = Elem<T>::BKE;
+  constexpr int HI = (kHaloPix + 8 * NW - 1) / (8 * NW);
+  constexpr int HROWS = HI * NW * 8;
+  constexpr int WI = BR / (8 * NW);
+  static_assert(WI >= 1 && BR % (8 * NW) == 0, "weight tile split");
+  constexpr int HALO_BYTES = HROWS * 128;
+  constexpr int WSLOT = BR * 128;
+  constexpr int WOFF = HB * HALO_BYTES;
+  constexpr int PARAM_OFF = WOFF + 3 * WSLOT;
+  __shared__ __attribute__((aligned(16))) char lds[PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4];
+  float* bias_s = reinterpret_cast<float*>(lds + PARAM_OFF);
+  float* headw_s = bias_s + BR;
+  float* headb_s = headw_s + kMaxClasses * 64;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wr = wave / WPX;
+  const int wp = wave % WPX;
+
+  int bid;
+  {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one pixel tile
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
+    const int b = blockIdx.x, x = b & 7, k = b >> 3;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  }
+  const int ct = bid % a.n_ct;
+  const int slot = bid / a.n_ct;
+  const int n_slots = gridDim.x / a.n_ct;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  if (slot >= n_mt) return;
+  const int items = (n_mt - slot + n_slots - 1) / n_slots;
+
+  const int H = a.H, W = a.W;
+  const int K = 9 * a.Cin;
+  const int nch = a.Cin / BKE;
+  const int S = 9 * nch;
+  const int total = items * S;
+  const int hseq_end = items * nch;
+
+  // per-block parameters into LDS (plain loads, before any DMA is in flight)
+  for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];
+  if (EPI == EPI_HEAD) {
+    for (int i = tid; i < a.ncls * 64; i += 64 * NW) headw_s[i] = a.head_w[i];
+    if (tid < a.ncls) headb_s[tid] = a.head_b[tid];
+  }
+  __syncthreads();
+
+  // halo rows owned by this lane: offsets of the halo pixel relative to the tile origin
+  int h_dy[HI], h_dx[HI], h_chk[HI];
+#pragma unroll
+  for (int j = 0; j < HI; ++j) {
+    const int row = (wave * HI + j) * 8 + (lane >> 3);
+    const int hy = row / 18, hx = row - (row / 18) * 18;
+    h_dy[j] = row < kHaloPix ? hy - 1 : -0x40000000;   // padding rows never valid
+    h_dx[j] = hx - 1;
+    h_chk[j] = ((lane & 7) ^ (hx & 7)) * 16;
+  }
+  const int w_chk = ((lane & 7) ^ ((lane >> 3) & 7)) * 16;
+  const char* wbase[WI];
+#pragma unroll
+  for (int j = 0; j < WI; ++j) {
+    const int row = (wave * WI + j) * 8 + (lane >> 3);
+    wbase[j] = reinterpret_cast<const char*>(a.wgt) + (size_t)(ct * BR + row) * K * sizeof(T) + w_chk;
+  }
+  const char* in = reinterpret_cast<const char*>(a.in);
+  const char* zero = reinterpret_cast<const char*>(a.zero);
+
+  auto tile_of = [&](int i, int& n, int& ty, int& tx) {
+    int mt = slot + i * n_slots;
+    tx = mt % a.tiles_x;
+    mt /= a.tiles_x;
+    ty = mt % a.tiles_y;
+    n = mt / a.tiles_y;
+  };
+  auto issue_halo = [&](int hseq) {
+    const int i = hseq / nch, c = hseq - (hseq / nch) * nch;
+    int n, ty, tx;
+    tile_of(i, n, ty, tx);
+    char* dst = lds + (HB == 2 ? (hseq & 1) * HALO_BYTES : 0) + wave * HI * 8 * 128;
+    const long long c0 = (long long)c * BKE;
+    const int pix0 = (n * H + ty * 16) * W + tx * 16;
+#pragma unroll
+    for (int j = 0; j < HI; ++j) {
+      const int iy = ty * 16 + h_dy[j], ix = tx * 16 + h_dx[j];
+      const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const long long pix = pix0 + h_dy[j] * W + h_dx[j];
+      const char* src = ok ? in + (pix * a.ldi + c0) * (long long)sizeof(T) + h_chk[j] : zero + h_chk[j];
+      glds16(src, dst + j * 8 * 128);
+    }
+  };
+  auto issue_w = [&](int g) {
+    const int s = g % S;
+    const int c = s / 9, tap = s - (s / 9) * 9;
+    const size_t koff = ((size_t)tap * a.Cin + (size_t)c * BKE) * sizeof(T);
+    char* dst = lds + WOFF + (g % 3) * WSLOT + wave * WI * 8 * 128;
+#pragma unroll
+    for (int j = 0; j < WI; ++j) glds16(wbase[j] + koff, dst + j * 8 * 128);
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int t = 0; t < TC; ++t)
+#pragma unroll
+    for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int col = lane & 15, q = lane >> 4;
+  int prow[TP];
 #pragma unroll
   for (int p = 0; p < TP; ++p) {
     int py, px;
-    pix_of(wp * TP * 16 + p * 16 + col, py, px);
-    const int oy = ty * TH + py, ox = tx * 16 + px;
-    const bool inside = oy < H && ox < W;
-    float v[16];
-#pragma unroll
-    for (int t = 0; t < TC; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = acc[t][p][e] + bv[t * 4 + e];
-        if (EPI != EPI_UPSCATTER) x = fmaxf(x, 0.f);
-        v[t * 4 + e] = x;
-      }
+    pix_of((wp * TP + p) * 16 + col, py, px);
+    prow[p] = py * 18 + px;
+  }
+  const int px_lane = col & 7;
 
-    if constexpr (EPI == EPI_STORE || EPI == EPI_POOL) {
-      if (inside) {
-        T* dst = reinterpret_cast<T*>(a.out) + ((long long)(n * H + oy) * W + ox) * a.ldo + a.out_off + rbase;
-        store16<T>(dst, v);
-      }
-      if constexpr (EPI == EPI_POOL) {
-        float m[16];
+  issue_halo(0);
+  issue_w(0);
+  if (total > 1) {
+    issue_w(1);
+    wait_vm_barrier<WI>();
+  } else {
+    wait_vm_barrier<0>();
+  }
+
+  int c = 0, tap = 0, hseq = 0, item = 0;
+  for (int g = 0; g < total; ++g) {
+    const bool hnext = (tap == 0) && (hseq + 1 < hseq_end);
+    const bool wnext = g + 2 < total;
+    if (hnext) issue_halo(hseq + 1);
+    if (wnext) issue_w(g + 2);
+
+    const int dy = tap / 3, dx = tap - (tap / 3) * 3;
+    const char* Hs = lds + (HB == 2 ? (hseq & 1) * HALO_BYTES : 0);
+    const char* Ws = lds + WOFF + (g % 3) * WSLOT + (wr * 64 + col) * 128;
+    const int toff = dy * 18 + dx;
+    const int hx7 = (px_lane + dx) & 7;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          float o = fmaxf(v[e], __shfl_xor(v[e], 1));
-          m[e] = fmaxf(o, __shfl_xor(o, 8));
-        }
-        if ((col & 9) == 0 && oy + 1 < H && ox + 1 < W) {
-          const int Ho = H >> 1, Wo = W >> 1;
-          T* dst = reinterpret_cast<T*>(a.out2) +
-                   ((long long)(n * Ho + (oy >> 1)) * Wo + (ox >> 1)) * a.ldo2 + rbase;
-          store16<T>(dst, m);
-        }
-      }
-    } else if constexpr (EPI == EPI_UPSCATTER) {
-      if (inside) {
-        const int ab = rbase / a.Cout;
-        const int o0 = rbase - ab * a.Cout;
-        const int Y = 2 * oy + (ab >> 1), X = 2 * ox + (ab & 1);
-        T* dst = reinterpret_cast<T*>(a.out) +
-                 ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0;
-        store16<T>(dst, v);
-      }
-    } else {  // EPI_HEAD: 1x1 conv 64 -> ncls on the fp32 activations, then masks
-      for (int c = 0; c < a.ncls; ++c) {
-        const float* hw = a.head_w + c * 64 + wr * 64 + q * 16;
-        float sum = 0.f;
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + q;
+      uint4 af[TC], bfv[TP];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) sum = fmaf(hw[e], v[e], sum);
-        sum += __shfl_xor(sum, 16);
-        sum += __shfl_xor(sum, 32);
-        const float logit = sum + a.head_b[c];
-        const long long pix = ((long long)(n * a.ncls + c) * H + oy) * W + ox;
-        if (a.logits && q == 0 && inside) a.logits[pix] = logit;
-        if (a.mask_kind != MASK_NONE) {
-          const float prob = 1.0f / (1.0f + expf(-logit));   // torch.sigmoid, inference.py:72
-          const bool on = prob > a.thr[c];                    // strict '>', inference.py:76-78
-          if (a.mask_kind == MASK_U8) {
-            if (q == 0 && inside) a.masks[pix] = on ? 1 : 0;
-          } else {
-            const unsigned long long bal = __ballot(on);
-            if (q == 0 && (col & 7) == 0 && inside) {
-              const unsigned byte = (unsigned)(bal >> (col & 8)) & 0xFFu;
-              a.masks[((long long)(n * a.ncls + c) * H + oy) * (W >> 3) + (ox >> 3)] = (uint8_t)byte;
-            }
-          }
-        }
+      for (int t = 0; t < TC; ++t)
+        af[t] = *reinterpret_cast<const uint4*>(Ws + t * 16 * 128 + ((chunk ^ (lane & 7)) << 4));
+#pragma unroll
+      for (int p = 0; p < TP; ++p)
+        bfv[p] = *reinterpret_cast<const uint4*>(Hs + (prow[p] + toff) * 128 + ((chunk ^ hx7) << 4));
+#pragma unroll
+      for (int t = 0; t < TC; ++t)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) mfma_frag<T>(acc[t][p], af[t], bfv[p]);
+    }
+    if (hnext) {
+      if (wnext) wait_vm_barrier<HI + WI>(); else wait_vm_barrier<HI>();
+    } else {
+      if (wnext) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
+    }
+
+    if (++tap == 9) {
+      tap = 0;
+      ++hseq;
+      if (++c == nch) {
+        c = 0;
+        int n, ty, tx;
+        tile_of(item, n, ty, tx);
+        conv_epilogue<T, TP, EPI>(a, acc, n, ty * 16, tx * 16, wp * TP, ct * BR + wr * 64,
+                                  bias_s + wr * 64, headw_s, headb_s);
+#pragma unroll
+        for (int t = 0; t < TC; ++t)
+#pragma unroll
+          for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ++item;
       }
     }
   }
@@ -372,8 +618,36 @@ static hipError_t launch_one(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <typename T, int WR, int WPX, int HB, int EPI>
+static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
+  // HB=2: persistent grid, n_ct row tiles x n_slots pixel-tile walkers, ~one block per CU.
+  // HB=1: one block per (row tile, pixel tile); only for a single 128-byte input chunk.
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  int n_slots = n_mt;
+  if (HB == 2) {
+    n_slots = kPersistBlocks / a.n_ct;
+    if (n_slots < 1) n_slots = 1;
+    if (n_slots > n_mt) n_slots = n_mt;
+  } else if (a.Cin != Elem<T>::BKE) {
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, HB, EPI>), dim3(a.n_ct * n_slots), dim3(64 * WR * WPX), 0, s, a);
+  return hipGetLastError();
+}
+
 template <typename T, int TAPS, int EPI>
 static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
+  if constexpr (TAPS == 9) {
+    switch (cfg) {
+      case CFG_HALO_R128_W4: return launch_halo<T, 2, 2, 2, EPI>(a, s);
+      case CFG_HALO_R128_W8: return launch_halo<T, 2, 4, 2, EPI>(a, s);
+      case CFG_HALO_R64_W4: return launch_halo<T, 1, 4, 2, EPI>(a, s);
+      case CFG_HALO_R64_W8: return launch_halo<T, 1, 8, 2, EPI>(a, s);
+      case CFG_HALO1_R64_W4: return launch_halo<T, 1, 4, 1, EPI>(a, s);
+      case CFG_HALO1_R64_W8: return launch_halo<T, 1, 8, 1, EPI>(a, s);
+      default: break;
+    }
+  }
   switch (cfg) {
     case CFG_R128_P128: return launch_one<T, 2, 2, 4, TAPS, EPI>(a, s);
     case CFG_R64_P128: return launch_one<T, 1, 4, 2, TAPS, EPI>(a, s);
@@ -389,7 +663,7 @@ static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipSt
       case EPI_STORE: return launch_cfg<T, 9, EPI_STORE>(cfg, a, s);
       case EPI_POOL: return launch_cfg<T, 9, EPI_POOL>(cfg, a, s);
       case EPI_HEAD:
-        if (cfg == CFG_R128_P128) return hipErrorInvalidValue;
+        if (cfg_rows(cfg) != 64) return hipErrorInvalidValue;
         return launch_cfg<T, 9, EPI_HEAD>(cfg, a, s);
       default: return hipErrorInvalidValue;
     }
