@@ -83,6 +83,24 @@ def launch_flops(entry, n, h, w, c_in, ncls=3):
     return f
 
 
+def launch_bytes(entry, n, h, w, c_in, esize, ncls=3):
+    """Algorithmic HBM bytes of one launch: every activation read once and written once,
+    weights read once, concat zero-copy, BN/ReLU/pool/head fused."""
+    name, _, cin, cout, lvl, kind = entry
+    hh, ww = h >> lvl, w >> lvl
+    if kind == "first":
+        return n * c_in * hh * ww * 4 + n * hh * ww * cout * esize + 9 * c_in * 64 * 4
+    if kind == "up":
+        return n * hh * ww * cin * esize + cin * 4 * cout * esize + n * 4 * hh * ww * cout * esize
+    b = n * hh * ww * cin * esize + 9 * cin * cout * esize
+    if name == "conv1.3":
+        return b + n * ncls * hh * ww // 8            # bit-packed masks only
+    b += n * hh * ww * cout * esize
+    if name.startswith("down") and name.endswith(".3"):
+        b += n * (hh // 2) * (ww // 2) * cout * esize  # fused max-pool output
+    return b
+
+
 def gen_pages(seed, batch, size, channels, unique=32):
     """Synthetic invoice pages; `unique` distinct pages tiled to the batch (generation cost)."""
     u = min(unique, batch)
@@ -170,14 +188,17 @@ def main():
     if not args.no_layer_profile:
         ms = handle.forward_timed(x, None, masks, native.MASK_BITS, stream)
         for entry, t in zip(LAUNCHES, ms):
-            k = kernels.setdefault(entry[1], {"launches": 0, "ms": 0.0, "gflop": 0.0})
+            k = kernels.setdefault(entry[1], {"launches": 0, "ms": 0.0, "gflop": 0.0, "algo_gb": 0.0})
             k["launches"] += 1
             k["ms"] += t
             k["gflop"] += launch_flops(entry, B, S, S, C) / 1e9
+            k["algo_gb"] += launch_bytes(entry, B, S, S, C, 4 if args.dtype == "fp32" else 2) / 1e9
         for k in kernels.values():
             k["tflops"] = round(k["gflop"] / k["ms"], 1) if k["ms"] > 0 else None
             k["ms"] = round(k["ms"], 3)
             k["gflop"] = round(k["gflop"], 1)
+            k["algo_gbs"] = round(k["algo_gb"] / k["ms"] * 1e3, 1) if k["ms"] > 0 else None
+            k["algo_gb"] = round(k["algo_gb"], 2)
         dom_name, dom = max(((n, k) for n, k in kernels.items() if n.startswith("igemm")), key=lambda kv: kv[1]["ms"])
         achieved = dom["gflop"] / dom["ms"]   # TFLOP/s (GFLOP / ms)
         peak = PEAK_TFLOPS[args.dtype]

@@ -168,3 +168,20 @@ def test_weight_update_repacks():
         b = m(x)
     assert torch.allclose(b - a, torch.ones_like(a), atol=1e-4)
     m.close()
+
+
+@pytest.mark.parametrize("cfg", list(range(11)))
+def test_every_kernel_config(cfg, monkeypatch):
+    """Each implicit-GEMM configuration (csrc/unet_internal.h Cfg) forced on every 3x3 layer
+    it supports, checked against the reference golden (fp32 and bf16)."""
+    monkeypatch.setenv("UNET_MI355X_CFG", ",".join(f"{i}:{cfg}" for i in range(17)))
+    z = np.load(os.path.join(GOLD, "unet_c3_h64w64_n2_structured.npz"))
+    sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile=str(z["profile"]))
+    for dtype in ("fp32", "bf16"):
+        m = make_model(sd, 3, dtype)
+        with torch.no_grad():
+            out = m(torch.from_numpy(z["x"]).to(DEV)).cpu().numpy()
+        err = rel_err(out, z["logits"])
+        print(f"cfg {cfg} {dtype}: rel err {err:.3e}")
+        assert err <= TOL[dtype]
+        m.close()

@@ -82,6 +82,7 @@ struct unet_handle {
   unet_config cfg{};
   DType dt = DType::BF16;
   float* w0 = nullptr;  // first conv folded fp32 [64][C][3][3]
+  void* w0p = nullptr;  // first conv packed [64][32] element type (16-bit MFMA path)
   float* b0 = nullptr;
   Layer L[17];          // d1b d2a d2b d3a d3b d4a d4b bna bnb c4a c4b c3a c3b c2a c2b c1a c1b
   Layer U[4];           // up4 up3 up2 up1
@@ -107,6 +108,19 @@ const int kLayerCh[17][2] = {{64, 64},    {64, 128},   {128, 128}, {128, 256}, {
                              {256, 512},  {512, 512},  {512, 1024}, {1024, 1024},
                              {1024, 512}, {512, 512},  {512, 256}, {256, 256},
                              {256, 128},  {128, 128},  {128, 64},  {64, 64}};
+// Default kernel configuration per 3x3 layer, from in-process A/B timing on MI355X at
+// bs256 512x512 bf16 (tools/tune.py; profiles/tune_r1.txt).  Two-blocks-per-CU halo tiles
+// (64 rows) win wherever the pixel grid is large relative to K; the persistent 128-row
+// halo kernel wins on the deep decoder convs.
+const int kDefaultCfg[17] = {
+    CFG_HALO1_R64_W8,                                       // down1.3 (+pool)
+    CFG_HALO1_R64_W4, CFG_HALO1_R64_W4, CFG_HALO1_R64_W4,    // down2.0 down2.3 down3.0
+    CFG_HALO1_R64_W4, CFG_HALO1_R64_W4, CFG_HALO1_R64_W4,    // down3.3 down4.0 down4.3
+    CFG_HALO1_R64_W4, CFG_HALO1_R64_W4,                      // bottleneck.0 .3
+    CFG_HALO_R128_W8, CFG_HALO_R128_W8,                      // conv4.0 conv4.3
+    CFG_HALO1_R64_W4, CFG_HALO_R128_W8,                      // conv3.0 conv3.3
+    CFG_HALO1_R64_W4, CFG_HALO_R128_W8,                      // conv2.0 conv2.3
+    CFG_HALO1_R64_W4, CFG_HALO1_R64_W8};                     // conv1.0, conv1.3 (+head)
 const char* kUpKey[4] = {"up4", "up3", "up2", "up1"};
 const int kUpCh[4][2] = {{1024, 512}, {512, 256}, {256, 128}, {128, 64}};
 
@@ -279,10 +293,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     L.taps = 9;
     if (ps == "gather") {
       L.cfg = L.cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
-    } else if (L.cout == 64) {
-      L.cfg = L.cin == chunk ? CFG_HALO1_R64_W8 : CFG_R64_P256;
     } else {
-      L.cfg = CFG_HALO_R128_W8;
+      L.cfg = kDefaultCfg[i];
     }
   }
   if (ps == "gather") h->L[C1B].cfg = CFG_R64_P128;
@@ -303,7 +315,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   }
   for (int i = 0; i < 17; ++i) {   // keep every layer on a configuration it supports
     Layer& L = h->L[i];
-    if (cfg_rows(L.cfg) > L.cout || (cfg_single_chunk(L.cfg) && L.cin != chunk))
+    if (cfg_rows(L.cfg) > L.cout || L.cfg == CFG_R128_P256 || (cfg_single_chunk(L.cfg) && L.cin != chunk))
       L.cfg = L.cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
     if (i == C1B && cfg_rows(L.cfg) != 64) L.cfg = CFG_R64_P128;
   }
@@ -350,6 +362,16 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
     rc = upload(h, (void**)&h->w0, wf.data(), wf.size() * 4);
     if (!rc) rc = upload(h, (void**)&h->b0, bf.data(), bf.size() * 4);
     if (rc) return rc;
+    h->w0p = nullptr;
+    if (h->dt != DType::F32) {   // MFMA operand: [rho][k], k = c*9 + ky*3 + kx < 9C, zero pad to 32
+      std::vector<uint8_t> pk((size_t)64 * 32 * 2, 0);
+      for (int rho = 0; rho < 64; ++rho) {
+        const int o = natural_of_packed(rho);
+        for (int k = 0; k < 9 * C; ++k) put_elem(h->dt, pk, (size_t)rho * 32 + k, w[(size_t)o * 9 * C + k]);
+      }
+      rc = upload(h, &h->w0p, pk.data(), pk.size());
+      if (rc) return rc;
+    }
   }
   for (int i = 0; i < 17; ++i) {
     rc = fold(sd, kLayerKey[i][0], kLayerKey[i][1], h->L[i].cin, h->L[i].cout, w, b);
@@ -467,6 +489,7 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   FirstConvArgs f{};
   f.x = static_cast<const float*>(x);
   f.w = h->w0;
+  f.wp = h->w0p;
   f.b = h->b0;
   f.out = buf(B.tA);
   f.N = N; f.C = h->cfg.n_channels; f.H = H; f.W = W;

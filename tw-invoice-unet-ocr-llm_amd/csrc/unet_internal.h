@@ -50,7 +50,9 @@ struct IgemmArgs {
 
 struct FirstConvArgs {
   const float* x;      // NCHW fp32 input [N][C][H][W]
-  const float* w;      // [64][C][3][3] folded
+  const float* w;      // [64][C][3][3] folded (fp32 VALU path)
+  const void* wp;      // [64][32] packed element type, k = c*9 + ky*3 + kx, zero-padded,
+                       // rows permuted like the implicit-GEMM weights (MFMA path)
   const float* b;      // [64] folded
   void* out;           // NHWC [N][H][W][64] element type T
   int N, C, H, W;
@@ -62,8 +64,9 @@ struct FirstConvArgs {
 enum Cfg : int {
   CFG_R128_P128 = 0, CFG_R64_P128 = 1, CFG_R64_P256 = 2, CFG_R128_P256 = 3,
   CFG_HALO_R128_W4 = 4, CFG_HALO_R128_W8 = 5, CFG_HALO_R64_W4 = 6, CFG_HALO_R64_W8 = 7,
-  CFG_HALO1_R64_W4 = 8, CFG_HALO1_R64_W8 = 9,   // single halo buffer, Cin == one 128-B chunk
-  CFG_COUNT = 10
+  CFG_HALO1_R64_W4 = 8, CFG_HALO1_R64_W8 = 9,   // single halo buffer, two blocks per CU
+  CFG_HALO1_R128_W4 = 10,                       // single halo buffer, 2-slot weight ring
+  CFG_COUNT = 11
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);

@@ -29,9 +29,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 int cfg_rows(int cfg) {
-  return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8) ? 128 : 64;
+  return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8 ||
+          cfg == CFG_HALO1_R128_W4) ? 128 : 64;
 }
-bool cfg_single_chunk(int cfg) { return cfg == CFG_HALO1_R64_W4 || cfg == CFG_HALO1_R64_W8; }
+bool cfg_single_chunk(int cfg) { (void)cfg; return false; }
 int cfg_pixels(int cfg) { return (cfg == CFG_R64_P128 || cfg == CFG_R128_P128) ? 128 : 256; }
 bool cfg_is_halo(int cfg) { return cfg >= CFG_HALO_R128_W4; }
 
@@ -373,14 +374,16 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
 }
 
-template <typename T, int WR, int WPX, int HB, int EPI>
+template <typename T, int WR, int WPX, int HB, int NS, int EPI>
 __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void conv3x3_halo_kernel(const IgemmArgs a) {
   // HB = 2 (persistent): gridDim.x = n_ct * n_slots blocks (host), each with a fixed row
   // tile ct, walks pixel tiles mt = slot, slot + n_slots, ...  The K-step pipeline (halo of
   // the next chunk, weights two steps ahead) runs continuously across tile boundaries, so
   // the next tile's loads overlap this tile's last steps and epilogue.
-  // HB = 1: one halo buffer, one tile per block, a single 64-channel chunk (Cin = BKE):
-  // small enough for two blocks per CU, which then overlap each other's epilogue.
+  // HB = 1: one halo buffer, one tile per block; the next chunk's halo is loaded after the
+  // last tap of the current one (an exposed load per chunk), but the block is small enough
+  // for two blocks per CU, which then cover each other's halo loads and epilogues.
+  // NS = weight-ring slots; weights are prefetched NS-1 steps ahead.
   constexpr int NW = WR * WPX;
   constexpr int TC = 4;
   constexpr int TP = 16 / WPX;
@@ -393,7 +396,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   constexpr int HALO_BYTES = HROWS * 128;
   constexpr int WSLOT = BR * 128;
   constexpr int WOFF = HB * HALO_BYTES;
-  constexpr int PARAM_OFF = WOFF + 3 * WSLOT;
+  constexpr int PARAM_OFF = WOFF + NS * WSLOT;
   __shared__ __attribute__((aligned(16))) char lds[PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4];
   float* bias_s = reinterpret_cast<float*>(lds + PARAM_OFF);
   float* headw_s = bias_s + BR;
@@ -480,7 +483,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     const int s = g % S;
     const int c = s / 9, tap = s - (s / 9) * 9;
     const size_t koff = ((size_t)tap * a.Cin + (size_t)c * BKE) * sizeof(T);
-    char* dst = lds + WOFF + (g % 3) * WSLOT + wave * WI * 8 * 128;
+    char* dst = lds + WOFF + (g % NS) * WSLOT + wave * WI * 8 * 128;
 #pragma unroll
     for (int j = 0; j < WI; ++j) glds16(wbase[j] + koff, dst + j * 8 * 128);
   };
@@ -503,7 +506,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
 
   issue_halo(0);
   issue_w(0);
-  if (total > 1) {
+  if (NS == 3 && total > 1) {
     issue_w(1);
     wait_vm_barrier<WI>();
   } else {
@@ -512,14 +515,14 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
 
   int c = 0, tap = 0, hseq = 0, item = 0;
   for (int g = 0; g < total; ++g) {
-    const bool hnext = (tap == 0) && (hseq + 1 < hseq_end);
-    const bool wnext = g + 2 < total;
+    const bool hnext = HB == 2 && (tap == 0) && (hseq + 1 < hseq_end);
+    const bool wnext = g + NS - 1 < total;
     if (hnext) issue_halo(hseq + 1);
-    if (wnext) issue_w(g + 2);
+    if (wnext) issue_w(g + NS - 1);
 
     const int dy = tap / 3, dx = tap - (tap / 3) * 3;
     const char* Hs = lds + (HB == 2 ? (hseq & 1) * HALO_BYTES : 0);
-    const char* Ws = lds + WOFF + (g % 3) * WSLOT + (wr * 64 + col) * 128;
+    const char* Ws = lds + WOFF + (g % NS) * WSLOT + (wr * 64 + col) * 128;
     const int toff = dy * 18 + dx;
     const int hx7 = (px_lane + dx) & 7;
 #pragma unroll
@@ -537,10 +540,17 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
 #pragma unroll
         for (int p = 0; p < TP; ++p) mfma_frag<T>(acc[t][p], af[t], bfv[p]);
     }
-    if (hnext) {
+    // the next step needs W(g+1) (and, at a chunk end, the next halo, which is older)
+    if (NS == 2) {
+      wait_vm_barrier<0>();
+    } else if (hnext) {
       if (wnext) wait_vm_barrier<HI + WI>(); else wait_vm_barrier<HI>();
     } else {
       if (wnext) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
+    }
+    if (HB == 1 && tap == 8 && hseq + 1 < hseq_end) {
+      issue_halo(hseq + 1);   // every wave has finished reading the halo (barrier above)
+      wait_vm_barrier<0>();
     }
 
     if (++tap == 9) {
@@ -609,6 +619,69 @@ __global__ __launch_bounds__(256) void first_conv_kernel(const FirstConvArgs a) 
   }
 }
 
+// First conv on MFMA (16-bit types): K = 9*C <= 27 padded to 32 = ONE 16x16x32 MFMA per
+// 16 pixels x 16 channels.  The fp32 input halo (18x18xC) is staged in LDS, B fragments are
+// built per lane from it, and the 64 output channels go through the shared epilogue
+// (bias + ReLU, 16-byte NHWC stores): the kernel is bound by the output write.
+template <typename T, int C>
+__global__ __launch_bounds__(256) void first_conv_mfma_kernel(const FirstConvArgs a, const IgemmArgs e) {
+  constexpr int KW = 9 * C;
+  __shared__ float xs[C * 18 * 18];
+  __shared__ float bias_s[64];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int H = a.H, W = a.W;
+  int mt = blockIdx.x;
+  const int tx = mt % e.tiles_x;
+  mt /= e.tiles_x;
+  const int ty = mt % e.tiles_y;
+  const int n = mt / e.tiles_y;
+  for (int i = tid; i < C * 324; i += 256) {
+    const int c = i / 324, r = i - c * 324, hy = r / 18, hx = r - (r / 18) * 18;
+    const int iy = ty * 16 + hy - 1, ix = tx * 16 + hx - 1;
+    const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+    xs[i] = ok ? a.x[(((long long)n * C + c) * H + iy) * W + ix] : 0.f;
+  }
+  if (tid < 64) bias_s[tid] = a.b[tid];
+  // A fragments (weights): row t*16 + (lane&15), k = 8*(lane>>4) .. +7
+  const int q = lane >> 4, col = lane & 15;
+  uint4 af[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    af[t] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.wp) + ((t * 16 + col) * 32 + 8 * q) * sizeof(T));
+  int koff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * q + j;
+    const int c = k / 9, r = k - (k / 9) * 9;
+    koff[j] = k < KW ? c * 324 + (r / 3) * 18 + (r - (r / 3) * 3) : -1;
+  }
+  __syncthreads();
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    int py, px;
+    pix_of((wave * 4 + p) * 16 + col, py, px);
+    const int base = py * 18 + px;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = koff[j] >= 0 ? xs[base + koff[j]] : 0.f;
+    uint4 bf;
+    if constexpr (sizeof(T) == 2) {
+      typedef T t8 __attribute__((ext_vector_type(8)));
+      t8 h;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) h[j] = (T)v[j];
+      bf = __builtin_bit_cast(uint4, h);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_frag<T>(acc[t][p], af[t], bf);
+    }
+  }
+  conv_epilogue<T, 4, EPI_STORE>(e, acc, n, ty * 16, tx * 16, wave * 4, 0, bias_s, nullptr, nullptr);
+}
+
 // ---------------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------------
@@ -618,20 +691,18 @@ static hipError_t launch_one(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int WR, int WPX, int HB, int EPI>
+template <typename T, int WR, int WPX, int HB, int NS, int EPI>
 static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   // HB=2: persistent grid, n_ct row tiles x n_slots pixel-tile walkers, ~one block per CU.
-  // HB=1: one block per (row tile, pixel tile); only for a single 128-byte input chunk.
+  // HB=1: one block per (row tile, pixel tile), two blocks per CU.
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
   int n_slots = n_mt;
   if (HB == 2) {
     n_slots = kPersistBlocks / a.n_ct;
     if (n_slots < 1) n_slots = 1;
     if (n_slots > n_mt) n_slots = n_mt;
-  } else if (a.Cin != Elem<T>::BKE) {
-    return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, HB, EPI>), dim3(a.n_ct * n_slots), dim3(64 * WR * WPX), 0, s, a);
+  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, HB, NS, EPI>), dim3(a.n_ct * n_slots), dim3(64 * WR * WPX), 0, s, a);
   return hipGetLastError();
 }
 
@@ -639,12 +710,13 @@ template <typename T, int TAPS, int EPI>
 static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
   if constexpr (TAPS == 9) {
     switch (cfg) {
-      case CFG_HALO_R128_W4: return launch_halo<T, 2, 2, 2, EPI>(a, s);
-      case CFG_HALO_R128_W8: return launch_halo<T, 2, 4, 2, EPI>(a, s);
-      case CFG_HALO_R64_W4: return launch_halo<T, 1, 4, 2, EPI>(a, s);
-      case CFG_HALO_R64_W8: return launch_halo<T, 1, 8, 2, EPI>(a, s);
-      case CFG_HALO1_R64_W4: return launch_halo<T, 1, 4, 1, EPI>(a, s);
-      case CFG_HALO1_R64_W8: return launch_halo<T, 1, 8, 1, EPI>(a, s);
+      case CFG_HALO_R128_W4: return launch_halo<T, 2, 2, 2, 3, EPI>(a, s);
+      case CFG_HALO_R128_W8: return launch_halo<T, 2, 4, 2, 3, EPI>(a, s);
+      case CFG_HALO_R64_W4: return launch_halo<T, 1, 4, 2, 3, EPI>(a, s);
+      case CFG_HALO_R64_W8: return launch_halo<T, 1, 8, 2, 3, EPI>(a, s);
+      case CFG_HALO1_R64_W4: return launch_halo<T, 1, 4, 1, 3, EPI>(a, s);
+      case CFG_HALO1_R64_W8: return launch_halo<T, 1, 8, 1, 3, EPI>(a, s);
+      case CFG_HALO1_R128_W4: return launch_halo<T, 2, 2, 1, 2, EPI>(a, s);
       default: break;
     }
   }
@@ -683,6 +755,21 @@ hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a,
 
 template <typename T>
 static hipError_t first_t(const FirstConvArgs& a, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    if (a.wp) {
+      IgemmArgs e{};
+      e.out = a.out;
+      e.N = a.N; e.H = a.H; e.W = a.W;
+      e.ldo = 64; e.out_off = 0;
+      e.tiles_x = (a.W + 15) / 16;
+      e.tiles_y = (a.H + 15) / 16;
+      const dim3 grid((unsigned)((long long)a.N * e.tiles_x * e.tiles_y));
+      if (a.C == 1) hipLaunchKernelGGL((first_conv_mfma_kernel<T, 1>), grid, dim3(256), 0, s, a, e);
+      else if (a.C == 3) hipLaunchKernelGGL((first_conv_mfma_kernel<T, 3>), grid, dim3(256), 0, s, a, e);
+      else return hipErrorInvalidValue;
+      return hipGetLastError();
+    }
+  }
   const long long total = (long long)a.N * a.H * a.W;
   const dim3 grid((unsigned)((total + 255) / 256));
   if (a.C == 1) hipLaunchKernelGGL((first_conv_kernel<T, 1>), grid, dim3(256), 0, s, a);
