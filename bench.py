@@ -16,6 +16,7 @@ mask IoU of the GPU masks against it), kernels (per-instantiation time breakdown
 from __future__ import annotations
 
 import argparse
+import re
 import json
 import os
 import sys
@@ -30,6 +31,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from unet_mi355x import native  # noqa: E402
+from unet_mi355x.dist import all_gather_rows  # noqa: E402
 from unet_mi355x import synthetic as syn  # noqa: E402
 from unet_mi355x.model import UNet  # noqa: E402
 
@@ -37,7 +39,8 @@ METRIC = "invoice masks/sec at 512x512 bs256, 1/2/4/8 MI355X; IoU vs CPU ref"
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
-# launch order of include/unet_mi355x.h: (name, kernel instantiation, cin, cout, level, kind)
+# launch order of include/unet_mi355x.h: (name, layer group, cin, cout, level, kind); the
+# kernel instantiation of each launch comes from the library (unet_launch_label)
 LAUNCHES = [
     ("down1.0", "first_conv", None, 64, 0, "first"),
     ("down1.3", "igemm_r64p256_pool", 64, 64, 0, "c3"),
@@ -62,11 +65,17 @@ LAUNCHES = [
     ("conv1.0", "igemm_r64p256_store", 128, 64, 0, "c3"),
     ("conv1.3", "igemm_r64p128_head", 64, 64, 0, "c3"),
 ]
-KERNEL_SYMBOL = {  # template arguments <T, WR, WPX, TP, TAPS, EPI> of unet::igemm_kernel
-    "igemm_r128p128_store": "2, 2, 4, 9, 0", "igemm_r128p128_pool": "2, 2, 4, 9, 1",
-    "igemm_r128p128_upscatter": "2, 2, 4, 1, 3", "igemm_r64p256_pool": "1, 4, 4, 9, 1",
-    "igemm_r64p256_store": "1, 4, 4, 9, 0", "igemm_r64p128_head": "1, 4, 2, 9, 2",
-}
+TYPE_CODE = {"float": "f", "__bf16": "DF16b", "_Float16": "DF16_"}
+
+
+def mangled(label):
+    """Itanium-mangled symbol of a "kernel<T, ints...>" label (what rocprofv3 may print)."""
+    m = re.match(r"(\w+)<([\w]+), ([\d, ]+)>$", label)
+    if not m:
+        return None
+    name, t, ints = m.group(1), m.group(2), [int(v) for v in m.group(3).split(", ")]
+    args = "".join(f"Li{v}E" for v in ints)
+    return f"_ZN4unet{len(name)}{name}I{TYPE_CODE[t]}{args}EEvNS_9IgemmArgsE"
 
 
 def launch_flops(entry, n, h, w, c_in, ncls=3):
@@ -130,8 +139,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if "RANK" in os.environ and "MASTER_ADDR" in os.environ:   # launched by torchrun
+        dist.init_process_group("nccl", device_id=dev)          # RCCL over xGMI
+    if args.gpus != world and rank == 0:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
 
     B, S, C = args.batch, args.size, args.channels
     # weights: structured synthetic (the real checkpoint is an LFS pointer); out_conv bias
@@ -141,10 +152,11 @@ def main():
     model.load_state_dict(sd)
     model = model.to(dev).eval()
     x = torch.from_numpy(gen_pages(1000 + rank, B, S, C)).to(dev)
-    with torch.no_grad():
-        lg = model(x[:2])
+    with torch.no_grad():   # full-batch forward: every profiled dispatch has the timed shape
+        lg = model(x)[:2]
     thr = torch.tensor([0.25, 0.40, 0.30], dtype=torch.float64)
     q = torch.quantile(lg.double().transpose(0, 1).reshape(3, -1).cpu(), 0.9, dim=1)
+    del lg
     shift = (torch.log(thr / (1 - thr)) - q).float()
     if world > 1:   # identical weights on every rank
         shift = shift.to(dev)
@@ -156,13 +168,12 @@ def main():
     handle.reserve(B, S, S)
 
     masks = torch.empty((B, 3, S, S // 8), dtype=torch.uint8, device=dev)
-    gathered = torch.empty((world * B, 3, S, S // 8), dtype=torch.uint8, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
         handle.forward(x, None, masks, native.MASK_BITS, stream)
-        if gathered is not None:
-            dist.all_gather_into_tensor(gathered, masks)
+        if world > 1:   # the one exchange step: RCCL all-gather of the bit-packed masks
+            all_gather_rows(masks, world * B)
 
     for _ in range(args.warmup):
         step()
@@ -184,34 +195,39 @@ def main():
     value = world * B * args.steps / elapsed
 
     # ---- per-launch HIP-event timing (same stream) -> dominant kernel roofline
-    kernels, roofline = {}, None
+    kernels, roofline, layer_ms = {}, None, {}
     if not args.no_layer_profile:
+        labels = handle.launch_labels()
         ms = handle.forward_timed(x, None, masks, native.MASK_BITS, stream)
-        for entry, t in zip(LAUNCHES, ms):
-            k = kernels.setdefault(entry[1], {"launches": 0, "ms": 0.0, "gflop": 0.0, "algo_gb": 0.0})
+        esize = 4 if args.dtype == "fp32" else 2
+        for entry, lab, t in zip(LAUNCHES, labels, ms):
+            layer_ms[entry[0]] = round(t, 3)
+            k = kernels.setdefault(lab, {"launches": 0, "ms": 0.0, "gflop": 0.0, "algo_gb": 0.0, "layers": []})
             k["launches"] += 1
             k["ms"] += t
             k["gflop"] += launch_flops(entry, B, S, S, C) / 1e9
-            k["algo_gb"] += launch_bytes(entry, B, S, S, C, 4 if args.dtype == "fp32" else 2) / 1e9
+            k["algo_gb"] += launch_bytes(entry, B, S, S, C, esize) / 1e9
+            k["layers"].append(entry[0])
+        dom_name, dom = max(((n, k) for n, k in kernels.items() if "first_conv" not in n),
+                            key=lambda kv: kv[1]["ms"])
+        achieved = dom["gflop"] / dom["ms"]   # TFLOP/s (GFLOP / ms)
         for k in kernels.values():
             k["tflops"] = round(k["gflop"] / k["ms"], 1) if k["ms"] > 0 else None
+            k["algo_gbs"] = round(k["algo_gb"] / k["ms"] * 1e3, 1) if k["ms"] > 0 else None
+            k["avg_launch_ms"] = round(k["ms"] / k["launches"], 4)
             k["ms"] = round(k["ms"], 3)
             k["gflop"] = round(k["gflop"], 1)
-            k["algo_gbs"] = round(k["algo_gb"] / k["ms"] * 1e3, 1) if k["ms"] > 0 else None
             k["algo_gb"] = round(k["algo_gb"], 2)
-        dom_name, dom = max(((n, k) for n, k in kernels.items() if n.startswith("igemm")), key=lambda kv: kv[1]["ms"])
-        achieved = dom["gflop"] / dom["ms"]   # TFLOP/s (GFLOP / ms)
         peak = PEAK_TFLOPS[args.dtype]
         traffic = None
         if args.traffic_json and os.path.exists(args.traffic_json):
             tj = json.load(open(args.traffic_json))
             traffic = tj.get(dom_name, {}).get("hbm_bytes_per_launch")
-        roofline = {"bound": "mfma", "kernel": dom_name,
-                    "symbol": f"unet::igemm_kernel<{ {'bf16': '__bf16', 'fp16': '_Float16', 'fp32': 'float'}[args.dtype]}, {KERNEL_SYMBOL[dom_name]}>",
+        roofline = {"bound": "mfma", "kernel": dom_name, "symbol": mangled(dom_name),
                     "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 4), "traffic": traffic,
-                    "launches_per_step": dom["launches"],
-                    "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
+                    "launches_per_step": dom["launches"], "avg_launch_ms": dom["avg_launch_ms"],
+                    "gflop_per_launch": round(dom["gflop"] / dom["launches"], 1),
                     "whole_step_tflops": round(sum(launch_flops(e, B, S, S, C) for e in LAUNCHES) / 1e9 /
                                                sum(ms), 1)}
 
@@ -247,10 +263,10 @@ def main():
                                    f"threshold bit-packed masks" + (" + RCCL all-gather" if world > 1 else ""),
                        "global_batch": world * B, "per_gpu_batch": B, "image": S,
                        "parallelism": f"dp{world}"},
-            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
+            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "layer_ms": layer_ms,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -104,6 +104,11 @@ int unet_forward(unet_handle* h, const void* x, int x_layout, int x_dtype,
 #define UNET_NUM_LAUNCHES 22
 int unet_num_launches(void);
 
+/* Kernel instantiation run by launch i of a forward (e.g.
+ * "conv3x3_halo_kernel<__bf16, 1, 4, 1, 3, 1>"), spelled like the demangled symbol that
+ * rocprofv3 reports; "" for a bad index. */
+const char* unet_launch_label(const unet_handle* h, int i);
+
 /* unet_forward, plus HIP-event timing of every launch on the given stream (ms, in the
  * order above, launch_ms[UNET_NUM_LAUNCHES]).  Synchronises on the stream; for
  * measurement only. */

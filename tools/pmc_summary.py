@@ -12,12 +12,26 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tw-invoice-unet-ocr-llm_amd"))
+
+
+TYPES = {"f": "float", "DF16b": "__bf16", "DF16_": "_Float16"}
+
+
+def label_of(name):
+    """Our mangled kernel symbol -> "kernel<T, ints...>" (bench.py / unet_launch_label spelling)."""
+    m = re.match(r"_ZN4unet(\d+)(\w+?)I(DF16b|DF16_|f)((?:Li\d+E)+)E", name)
+    if not m:
+        return name
+    kname = m.group(2)[:int(m.group(1))]
+    ints = re.findall(r"Li(\d+)E", m.group(4))
+    return f"{kname}<{TYPES[m.group(3)]}, {', '.join(ints)}>"
 
 
 def load_pass(d):
@@ -65,7 +79,7 @@ def main():
         wait = 100 * c.get("SQ_WAIT_ANY", 0) / max(1, c.get("SQ_WAVE_CYCLES", 0))
         algo = launch_bytes(e, a.batch, a.size, a.size, 3, a.esize)
         print(f"{e[0]:14s} {rd / 1e9:8.2f} {wr / 1e9:8.2f} {algo / 1e9:8.2f} {mfma_pct:10.1f} {conf:9.2f} {wait:9.1f}")
-        k = agg[e[1]]
+        k = agg[label_of(c.get("kernel_name", e[1]))]
         k["launches"] += 1
         k["hbm_read_bytes"] += rd
         k["hbm_write_bytes"] += wr

@@ -6,12 +6,18 @@ The bench process also runs small warm-up / bias-centring forwards; grouping by 
 separates the full-batch dispatches (the ones bench.py's roofline times) from those.
 """
 import argparse
+import os
+import sys
 import csv
 import re
 from collections import defaultdict
 
 
 def short(name):
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pmc_summary import label_of
+    if name.startswith("_ZN4unet"):
+        return label_of(name)
     m = re.search(r"igemm_kernelI(\w+?)Li(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)E", name)
     if m:
         return f"igemm<{m.group(1)},{','.join(m.group(i) for i in range(2, 7))}>"

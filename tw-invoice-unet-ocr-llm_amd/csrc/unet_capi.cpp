@@ -8,6 +8,7 @@
 #include "../../include/unet_mi355x.h"
 
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -94,6 +95,7 @@ struct unet_handle {
   size_t ws_bytes = 0;
   int lastN = 0, lastH = 0, lastW = 0;
   std::vector<void*> allocs;
+  std::string labels[UNET_NUM_LAUNCHES];   // kernel instantiation of every launch
 };
 
 namespace {
@@ -264,6 +266,47 @@ int check_geometry(const unet_handle* h, int N, int H, int W) {
 
 }  // namespace
 
+namespace {
+const char* tname(DType t) { return t == DType::F32 ? "float" : t == DType::BF16 ? "__bf16" : "_Float16"; }
+
+// "kernel<template args>" of a layer, in the same spelling as the demangled symbol
+std::string layer_label(DType t, int cfg, int taps, int epi) {
+  char buf[128];
+  struct { int wr, wpx, tc, hb, ns, pipe; } halo[] = {
+      {2, 2, 4, 2, 3, 0}, {2, 4, 4, 2, 3, 0}, {1, 4, 4, 2, 3, 0}, {1, 8, 4, 2, 3, 0}, {1, 4, 4, 1, 3, 0},
+      {1, 8, 4, 1, 3, 0}, {2, 2, 4, 1, 2, 0}, {2, 4, 4, 2, 3, 1}, {1, 4, 4, 1, 3, 1}, {1, 8, 4, 1, 3, 1},
+      {1, 4, 8, 1, 2, 0}, {1, 4, 8, 1, 3, 0}};
+  if (cfg >= CFG_COUNT) {
+    std::snprintf(buf, sizeof buf, "ablation_%d<%s, %d>", cfg - CFG_COUNT, tname(t), epi);
+  } else if (cfg_is_halo(cfg)) {
+    const auto& c = halo[cfg - CFG_HALO_R128_W4];
+    std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, %d, %d, %d, %d, %d, %d, %d>", tname(t), c.wr, c.wpx,
+                  c.tc, c.hb, c.ns, c.pipe, epi);
+  } else {
+    const int wr = cfg_rows(cfg) / 64, wpx = 4 / wr, tp = cfg_pixels(cfg) / (16 * wpx);
+    std::snprintf(buf, sizeof buf, "igemm_kernel<%s, %d, %d, %d, %d, %d>", tname(t), wr, wpx, tp, taps, epi);
+  }
+  return buf;
+}
+
+void build_labels(unet_handle* h) {
+  const int C = h->cfg.n_channels;
+  char buf[96];
+  std::snprintf(buf, sizeof buf, h->dt == DType::F32 ? "first_conv_kernel<%s, %d>" : "first_conv_mfma_kernel<%s, %d>",
+                tname(h->dt), C);
+  // launch order (include/unet_mi355x.h): first, d1b .. bnb, up4, c4a, c4b, up3, c3a, c3b, up2, c2a, c2b, up1, c1a, c1b
+  const int order[UNET_NUM_LAUNCHES] = {-1, D1B, D2A, D2B, D3A, D3B, D4A, D4B, BNA, BNB, 100, C4A, C4B,
+                                        101, C3A, C3B, 102, C2A, C2B, 103, C1A, C1B};
+  for (int i = 0; i < UNET_NUM_LAUNCHES; ++i) {
+    const int id = order[i];
+    if (id < 0) { h->labels[i] = buf; continue; }
+    if (id >= 100) { h->labels[i] = layer_label(h->dt, h->U[id - 100].cfg, 1, EPI_UPSCATTER); continue; }
+    const int epi = id == C1B ? EPI_HEAD : (id == D1B || id == D2B || id == D3B || id == D4B) ? EPI_POOL : EPI_STORE;
+    h->labels[i] = layer_label(h->dt, h->L[id].cfg, 9, epi);
+  }
+}
+}  // namespace
+
 extern "C" {
 
 const char* unet_last_error(void) { return g_err.c_str(); }
@@ -308,7 +351,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
       const size_t colon = item.find(':');
       if (colon != std::string::npos) {
         const int li = std::atoi(item.substr(0, colon).c_str()), c = std::atoi(item.substr(colon + 1).c_str());
-        if (li >= 0 && li < 17 && c >= 0 && c < CFG_COUNT) h->L[li].cfg = c;
+        if (li >= 0 && li < 17 && c >= 0 && c < cfg_limit()) h->L[li].cfg = c;
       }
       pos = end + 1;
     }
@@ -319,6 +362,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
       L.cfg = L.cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
     if (i == C1B && cfg_rows(L.cfg) != 64) L.cfg = CFG_R64_P128;
   }
+  build_labels(h);
   for (int i = 0; i < 4; ++i) {
     h->U[i].cin = kUpCh[i][0];
     h->U[i].cout = kUpCh[i][1];
@@ -539,6 +583,11 @@ int unet_forward(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
 }
 
 int unet_num_launches(void) { return UNET_NUM_LAUNCHES; }
+
+const char* unet_launch_label(const unet_handle* h, int i) {
+  if (!h || i < 0 || i >= UNET_NUM_LAUNCHES) return "";
+  return h->labels[i].c_str();
+}
 
 int unet_forward_timed(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
                        int mask_kind, int N, int H, int W, void* stream, float* launch_ms) {

@@ -66,12 +66,17 @@ enum Cfg : int {
   CFG_HALO_R128_W4 = 4, CFG_HALO_R128_W8 = 5, CFG_HALO_R64_W4 = 6, CFG_HALO_R64_W8 = 7,
   CFG_HALO1_R64_W4 = 8, CFG_HALO1_R64_W8 = 9,   // single halo buffer, two blocks per CU
   CFG_HALO1_R128_W4 = 10,                       // single halo buffer, 2-slot weight ring
-  CFG_COUNT = 11
+  // software-pipelined fragment reads (next kk / next step read behind the MFMAs)
+  CFG_PHALO_R128_W8 = 11, CFG_PHALO1_R64_W4 = 12, CFG_PHALO1_R64_W8 = 13,
+  // 128-row x 64-pixel wave tiles (4 waves, 128 x 256 block), single halo buffer
+  CFG_HALO1_R128T8_NS2 = 14, CFG_HALO1_R128T8_NS3 = 15,
+  CFG_COUNT = 16
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);
 int cfg_pixels(int cfg);
 bool cfg_is_halo(int cfg);
+int cfg_limit();   // number of valid Cfg values in this build
 
 hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s);
 hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s);

@@ -27,14 +27,26 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef int frag_t __attribute__((ext_vector_type(4)));   // one 16-byte MFMA operand fragment
 
 int cfg_rows(int cfg) {
+#ifdef UNET_ABLATION
+  if (cfg >= CFG_COUNT) return (cfg == CFG_COUNT + 2 || cfg == CFG_COUNT + 3) ? 128 : 64;
+#endif
   return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8 ||
-          cfg == CFG_HALO1_R128_W4) ? 128 : 64;
+          cfg == CFG_HALO1_R128_W4 || cfg == CFG_PHALO_R128_W8 || cfg == CFG_HALO1_R128T8_NS2 ||
+          cfg == CFG_HALO1_R128T8_NS3) ? 128 : 64;
 }
 bool cfg_single_chunk(int cfg) { (void)cfg; return false; }
 int cfg_pixels(int cfg) { return (cfg == CFG_R64_P128 || cfg == CFG_R128_P128) ? 128 : 256; }
 bool cfg_is_halo(int cfg) { return cfg >= CFG_HALO_R128_W4; }
+int cfg_limit() {
+#ifdef UNET_ABLATION
+  return CFG_COUNT + 7;
+#else
+  return CFG_COUNT;
+#endif
+}
 
 // ---------------------------------------------------------------------------------
 // element traits
@@ -102,7 +114,9 @@ __device__ __forceinline__ void store16<_Float16>(_Float16* dst, const float (&v
 // lds_dst + 16*l.  Issued from inline asm on purpose: hipcc would otherwise treat every
 // later ds_read as aliasing the in-flight DMA and drain vmcnt(0) in front of it, which
 // serialises the load of step s+2 behind the compute of step s.  The waits are ours
-// (counted vmcnt before each barrier); M0 is saved/restored inside the statement.
+// (counted vmcnt before each barrier); M0 is saved/restored inside the statement.  No
+// "memory" clobber: the DMA never targets an LDS slot read in the same step, and the
+// barriers (volatile asm + memory clobber) keep it inside its step.
 __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
   const uint32_t lds_addr = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_t)lds_dst)));
@@ -114,8 +128,7 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
       "global_load_lds_dwordx4 %1, off\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(src), "s"(lds_addr)
-      : "memory");
+      : "v"(src), "s"(lds_addr));
 }
 
 // Pixel p (0..BP-1) of a block tile -> (row, col) inside the TH x 16 tile.  Pixels come
@@ -369,12 +382,19 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IgemmArgs a) {
 constexpr int kHaloPix = 18 * 18;
 constexpr int kPersistBlocks = 256;   // one resident block per CU (LDS-limited)
 
+// s_waitcnt vmcnt(N) lgkmcnt(0) + s_barrier.  The wait goes through the builtin (not asm) so
+// hipcc's waitcnt tracker knows every LDS read is retired here and does not re-wait for
+// them after the barrier; the empty asm statements keep memory operations from moving across.
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));   // vmcnt(N) expcnt(7) lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
-template <typename T, int WR, int WPX, int HB, int NS, int EPI>
+template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int EPI>
 __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void conv3x3_halo_kernel(const IgemmArgs a) {
   // HB = 2 (persistent): gridDim.x = n_ct * n_slots blocks (host), each with a fixed row
   // tile ct, walks pixel tiles mt = slot, slot + n_slots, ...  The K-step pipeline (halo of
@@ -384,10 +404,11 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   // last tap of the current one (an exposed load per chunk), but the block is small enough
   // for two blocks per CU, which then cover each other's halo loads and epilogues.
   // NS = weight-ring slots; weights are prefetched NS-1 steps ahead.
+  // TCW = 16-row MFMA tiles per wave (4: 64 rows, 8: 128 rows = two 64-row epilogue groups).
   constexpr int NW = WR * WPX;
-  constexpr int TC = 4;
+  constexpr int TC = TCW;
   constexpr int TP = 16 / WPX;
-  constexpr int BR = WR * 64;
+  constexpr int BR = WR * 16 * TC;
   constexpr int BKE = Elem<T>::BKE;
   constexpr int HI = (kHaloPix + 8 * NW - 1) / (8 * NW);
   constexpr int HROWS = HI * NW * 8;
@@ -436,23 +457,12 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   }
   __syncthreads();
 
-  // halo rows owned by this lane: offsets of the halo pixel relative to the tile origin
-  int h_dy[HI], h_dx[HI], h_chk[HI];
-#pragma unroll
-  for (int j = 0; j < HI; ++j) {
-    const int row = (wave * HI + j) * 8 + (lane >> 3);
-    const int hy = row / 18, hx = row - (row / 18) * 18;
-    h_dy[j] = row < kHaloPix ? hy - 1 : -0x40000000;   // padding rows never valid
-    h_dx[j] = hx - 1;
-    h_chk[j] = ((lane & 7) ^ (hx & 7)) * 16;
-  }
+  // Halo rows owned by this lane are recomputed at every (once-per-chunk) halo issue
+  // instead of being kept in ~3*HI registers; weight rows: one base pointer per lane.
   const int w_chk = ((lane & 7) ^ ((lane >> 3) & 7)) * 16;
-  const char* wbase[WI];
-#pragma unroll
-  for (int j = 0; j < WI; ++j) {
-    const int row = (wave * WI + j) * 8 + (lane >> 3);
-    wbase[j] = reinterpret_cast<const char*>(a.wgt) + (size_t)(ct * BR + row) * K * sizeof(T) + w_chk;
-  }
+  const char* wbase = reinterpret_cast<const char*>(a.wgt) +
+                      (size_t)(ct * BR + wave * WI * 8 + (lane >> 3)) * K * sizeof(T) + w_chk;
+  const size_t wstep = (size_t)8 * K * sizeof(T);   // 8 rows per DMA instruction
   const char* in = reinterpret_cast<const char*>(a.in);
   const char* zero = reinterpret_cast<const char*>(a.zero);
 
@@ -469,13 +479,16 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     tile_of(i, n, ty, tx);
     char* dst = lds + (HB == 2 ? (hseq & 1) * HALO_BYTES : 0) + wave * HI * 8 * 128;
     const long long c0 = (long long)c * BKE;
-    const int pix0 = (n * H + ty * 16) * W + tx * 16;
+    const long long pix0 = (long long)(n * H + ty * 16) * W + tx * 16;
 #pragma unroll
     for (int j = 0; j < HI; ++j) {
-      const int iy = ty * 16 + h_dy[j], ix = tx * 16 + h_dx[j];
-      const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      const long long pix = pix0 + h_dy[j] * W + h_dx[j];
-      const char* src = ok ? in + (pix * a.ldi + c0) * (long long)sizeof(T) + h_chk[j] : zero + h_chk[j];
+      const int row = (wave * HI + j) * 8 + (lane >> 3);
+      const int hy = row / 18, hx = row - hy * 18;
+      const int iy = ty * 16 + hy - 1, ix = tx * 16 + hx - 1;
+      const bool ok = row < kHaloPix && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const int chk = ((lane & 7) ^ (hx & 7)) * 16;
+      const long long pix = pix0 + (long long)(hy - 1) * W + (hx - 1);
+      const char* src = ok ? in + (pix * a.ldi + c0) * (long long)sizeof(T) + chk : zero + chk;
       glds16(src, dst + j * 8 * 128);
     }
   };
@@ -485,7 +498,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     const size_t koff = ((size_t)tap * a.Cin + (size_t)c * BKE) * sizeof(T);
     char* dst = lds + WOFF + (g % NS) * WSLOT + wave * WI * 8 * 128;
 #pragma unroll
-    for (int j = 0; j < WI; ++j) glds16(wbase[j] + koff, dst + j * 8 * 128);
+    for (int j = 0; j < WI; ++j) glds16(wbase + koff + j * wstep, dst + j * 8 * 128);
   };
 
   f32x4 acc[TC][TP];
@@ -513,35 +526,66 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     wait_vm_barrier<0>();
   }
 
+  // fragment reads of (step, kk) into a register set
+  auto read_frags = [&](int g, int hs, int tp, int kk, frag_t (&af)[TC], frag_t (&bf)[TP]) {
+    const int dy = tp / 3, dx = tp - (tp / 3) * 3;
+    const char* Hs = lds + (HB == 2 ? (hs & 1) * HALO_BYTES : 0);
+    const char* Ws = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 128;
+    const int toff = dy * 18 + dx;
+    const int hx7 = (px_lane + dx) & 7;
+    const int chunk = kk * 4 + q;
+#pragma unroll
+    for (int t = 0; t < TC; ++t)
+      af[t] = *reinterpret_cast<const frag_t*>(Ws + t * 16 * 128 + ((chunk ^ (lane & 7)) << 4));
+#pragma unroll
+    for (int p = 0; p < TP; ++p)
+      bf[p] = *reinterpret_cast<const frag_t*>(Hs + (prow[p] + toff) * 128 + ((chunk ^ hx7) << 4));
+  };
+  auto mfmas = [&](const frag_t (&af)[TC], const frag_t (&bf)[TP]) {
+#pragma unroll
+    for (int t = 0; t < TC; ++t)
+#pragma unroll
+      for (int p = 0; p < TP; ++p)
+        if constexpr (PIPE == 2) asm volatile("" ::"v"(af[t]), "v"(bf[p]));   // ablation: no MFMA
+        else mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af[t]), __builtin_bit_cast(uint4, bf[p]));
+  };
+  // after the barrier (which retired every LDS read with lgkmcnt(0)), declare the kk=1
+  // fragments "re-defined" so hipcc does not re-wait for their reads behind the next
+  // step's kk=0 reads (its waitcnt tracker does not model the barrier's wait)
+  auto reg_fence = [&](frag_t (&af)[TC], frag_t (&bf)[TP]) {
+#pragma unroll
+    for (int t = 0; t < TC; ++t) asm volatile("" : "+v"(af[t]) : : "memory");
+#pragma unroll
+    for (int p = 0; p < TP; ++p) asm volatile("" : "+v"(bf[p]) : : "memory");
+  };
+  frag_t a0[TC], b0[TP], a1[TC], b1[TP];
+  if (PIPE == 1 || PIPE == 5) read_frags(0, 0, 0, 0, a0, b0);
+
   int c = 0, tap = 0, hseq = 0, item = 0;
   for (int g = 0; g < total; ++g) {
     const bool hnext = HB == 2 && (tap == 0) && (hseq + 1 < hseq_end);
     const bool wnext = g + NS - 1 < total;
-    if (hnext) issue_halo(hseq + 1);
-    if (wnext) issue_w(g + NS - 1);
+    constexpr bool kDma = PIPE < 3;       // ablations 3, 4, 5: no DMA in the loop
+    constexpr bool kPipe = PIPE == 1 || PIPE == 5;
+    if (kDma && hnext) issue_halo(hseq + 1);
+    if (kDma && wnext) issue_w(g + NS - 1);
 
-    const int dy = tap / 3, dx = tap - (tap / 3) * 3;
-    const char* Hs = lds + (HB == 2 ? (hseq & 1) * HALO_BYTES : 0);
-    const char* Ws = lds + WOFF + (g % NS) * WSLOT + (wr * 64 + col) * 128;
-    const int toff = dy * 18 + dx;
-    const int hx7 = (px_lane + dx) & 7;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + q;
-      uint4 af[TC], bfv[TP];
-#pragma unroll
-      for (int t = 0; t < TC; ++t)
-        af[t] = *reinterpret_cast<const uint4*>(Ws + t * 16 * 128 + ((chunk ^ (lane & 7)) << 4));
-#pragma unroll
-      for (int p = 0; p < TP; ++p)
-        bfv[p] = *reinterpret_cast<const uint4*>(Hs + (prow[p] + toff) * 128 + ((chunk ^ hx7) << 4));
-#pragma unroll
-      for (int t = 0; t < TC; ++t)
-#pragma unroll
-        for (int p = 0; p < TP; ++p) mfma_frag<T>(acc[t][p], af[t], bfv[p]);
+    if (kPipe) {
+      // kk=1 reads in flight behind the kk=0 MFMAs; kk=0 of the next step is read right
+      // after the barrier, behind this step's kk=1 MFMAs: no read-latency bubble per step.
+      read_frags(g, hseq, tap, 1, a1, b1);
+      mfmas(a0, b0);
+    } else {
+      read_frags(g, hseq, tap, 0, a0, b0);
+      mfmas(a0, b0);
+      read_frags(g, hseq, tap, 1, a1, b1);
+      mfmas(a1, b1);
     }
-    // the next step needs W(g+1) (and, at a chunk end, the next halo, which is older)
-    if (NS == 2) {
+    // the next step needs W(g+1) (and, at a chunk end, the next halo, which is older);
+    // the barrier's lgkmcnt(0) also retires every fragment read of this step (WAR)
+    if (PIPE == 4) {
+      // ablation: no barrier
+    } else if (NS == 2) {
       wait_vm_barrier<0>();
     } else if (hnext) {
       if (wnext) wait_vm_barrier<HI + WI>(); else wait_vm_barrier<HI>();
@@ -549,25 +593,39 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
       if (wnext) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
     }
     if (HB == 1 && tap == 8 && hseq + 1 < hseq_end) {
-      issue_halo(hseq + 1);   // every wave has finished reading the halo (barrier above)
+      if (kDma) issue_halo(hseq + 1);   // every wave has finished reading the halo (barrier above)
       wait_vm_barrier<0>();
     }
 
+    bool tile_end = false;
     if (++tap == 9) {
       tap = 0;
       ++hseq;
       if (++c == nch) {
         c = 0;
-        int n, ty, tx;
-        tile_of(item, n, ty, tx);
-        conv_epilogue<T, TP, EPI>(a, acc, n, ty * 16, tx * 16, wp * TP, ct * BR + wr * 64,
-                                  bias_s + wr * 64, headw_s, headb_s);
-#pragma unroll
-        for (int t = 0; t < TC; ++t)
-#pragma unroll
-          for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-        ++item;
+        tile_end = true;
       }
+    }
+    if (kPipe) {
+      reg_fence(a1, b1);
+      // unconditional (clamped) so there is no control-flow merge in front of the MFMAs:
+      // hipcc's waitcnt tracker would otherwise re-wait for this step's retired reads
+      read_frags(g + 1 < total ? g + 1 : g, hseq, tap, 0, a0, b0);
+      mfmas(a1, b1);
+    }
+    if (tile_end) {
+      int n, ty, tx;
+      tile_of(item, n, ty, tx);
+#pragma unroll
+      for (int h = 0; h < TC / 4; ++h)
+        conv_epilogue<T, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
+                                  wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h,
+                                  headw_s, headb_s);
+#pragma unroll
+      for (int t = 0; t < TC; ++t)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ++item;
     }
   }
 }
@@ -691,7 +749,7 @@ static hipError_t launch_one(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int WR, int WPX, int HB, int NS, int EPI>
+template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int EPI>
 static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   // HB=2: persistent grid, n_ct row tiles x n_slots pixel-tile walkers, ~one block per CU.
   // HB=1: one block per (row tile, pixel tile), two blocks per CU.
@@ -702,7 +760,8 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
     if (n_slots < 1) n_slots = 1;
     if (n_slots > n_mt) n_slots = n_mt;
   }
-  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, HB, NS, EPI>), dim3(a.n_ct * n_slots), dim3(64 * WR * WPX), 0, s, a);
+  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, HB, NS, PIPE, EPI>), dim3(a.n_ct * n_slots),
+                     dim3(64 * WR * WPX), 0, s, a);
   return hipGetLastError();
 }
 
@@ -710,13 +769,27 @@ template <typename T, int TAPS, int EPI>
 static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
   if constexpr (TAPS == 9) {
     switch (cfg) {
-      case CFG_HALO_R128_W4: return launch_halo<T, 2, 2, 2, 3, EPI>(a, s);
-      case CFG_HALO_R128_W8: return launch_halo<T, 2, 4, 2, 3, EPI>(a, s);
-      case CFG_HALO_R64_W4: return launch_halo<T, 1, 4, 2, 3, EPI>(a, s);
-      case CFG_HALO_R64_W8: return launch_halo<T, 1, 8, 2, 3, EPI>(a, s);
-      case CFG_HALO1_R64_W4: return launch_halo<T, 1, 4, 1, 3, EPI>(a, s);
-      case CFG_HALO1_R64_W8: return launch_halo<T, 1, 8, 1, 3, EPI>(a, s);
-      case CFG_HALO1_R128_W4: return launch_halo<T, 2, 2, 1, 2, EPI>(a, s);
+      case CFG_HALO_R128_W4: return launch_halo<T, 2, 2, 4, 2, 3, 0, EPI>(a, s);
+      case CFG_HALO_R128_W8: return launch_halo<T, 2, 4, 4, 2, 3, 0, EPI>(a, s);
+      case CFG_HALO_R64_W4: return launch_halo<T, 1, 4, 4, 2, 3, 0, EPI>(a, s);
+      case CFG_HALO_R64_W8: return launch_halo<T, 1, 8, 4, 2, 3, 0, EPI>(a, s);
+      case CFG_HALO1_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 0, EPI>(a, s);
+      case CFG_HALO1_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 0, EPI>(a, s);
+      case CFG_HALO1_R128_W4: return launch_halo<T, 2, 2, 4, 1, 2, 0, EPI>(a, s);
+      case CFG_PHALO_R128_W8: return launch_halo<T, 2, 4, 4, 2, 3, 1, EPI>(a, s);
+      case CFG_PHALO1_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 1, EPI>(a, s);
+      case CFG_PHALO1_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 1, EPI>(a, s);
+      case CFG_HALO1_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 0, EPI>(a, s);
+      case CFG_HALO1_R128T8_NS3: return launch_halo<T, 1, 4, 8, 1, 3, 0, EPI>(a, s);
+#ifdef UNET_ABLATION   // timing-only builds: wrong outputs by construction
+      case CFG_COUNT + 0: return launch_halo<T, 1, 4, 4, 1, 3, 2, EPI>(a, s);   // HALO1_R64_W4, no MFMA
+      case CFG_COUNT + 1: return launch_halo<T, 1, 4, 4, 1, 3, 3, EPI>(a, s);   // HALO1_R64_W4, no DMA
+      case CFG_COUNT + 2: return launch_halo<T, 2, 4, 4, 2, 3, 2, EPI>(a, s);   // HALO_R128_W8, no MFMA
+      case CFG_COUNT + 3: return launch_halo<T, 2, 4, 4, 2, 3, 3, EPI>(a, s);   // HALO_R128_W8, no DMA
+      case CFG_COUNT + 4: return launch_halo<T, 1, 4, 4, 1, 3, 4, EPI>(a, s);   // HALO1_R64_W4, no DMA, no barrier
+      case CFG_COUNT + 5: return launch_halo<T, 1, 4, 4, 1, 3, 5, EPI>(a, s);   // PHALO1_R64_W4, no DMA
+      case CFG_COUNT + 6: return launch_halo<T, 1, 4, 4, 1, 3, 1, EPI>(a, s);   // PHALO1_R64_W4 (same binary A/B)
+#endif
       default: break;
     }
   }

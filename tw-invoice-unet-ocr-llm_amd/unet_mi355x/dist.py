@@ -1,0 +1,83 @@
+"""Batch data-parallel inference across the GPUs of one node.
+
+Images are independent (eval-mode BatchNorm, no cross-batch coupling), so a global batch is
+split contiguously over ranks -- one process per GPU, rank r gets
+[r*N/P, (r+1)*N/P) -- every rank runs the native forward on its shard with a full weight
+replica, and the only exchange step is ONE all-gather of the (bit-packed) masks.  With the
+"nccl" backend that collective is RCCL over xGMI; with "gloo" (CPU tests) it is the same
+code path.  The reference has no parallelism at all (single device, inference.py:9).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n_total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous shard [lo, hi) of rank; the first n_total % world ranks get one extra."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    base, extra = divmod(n_total, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def _backend(group=None) -> str:
+    return dist.get_backend(group) if dist.is_initialized() else "none"
+
+
+def all_gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
+    """Gather the per-rank shards (dim 0, sizes per shard_bounds) into the full batch.
+
+    Shards are padded to the largest shard so one all_gather_into_tensor covers ragged
+    batches; the padding is dropped on return.  Order = rank order = original batch order.
+    """
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = shard_bounds(n_total, rank, world)
+    if local.shape[0] != hi - lo:
+        raise ValueError(f"rank {rank}: local shard has {local.shape[0]} rows, expected {hi - lo}")
+    cap = shard_bounds(n_total, 0, world)[1]          # largest shard (rank 0)
+    if local.shape[0] < cap:
+        pad = torch.zeros((cap - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        send = torch.cat([local, pad], 0)
+    else:
+        send = local.contiguous()
+    out = torch.empty((world * cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if _backend(group) == "gloo":
+        parts = list(out.chunk(world, 0))
+        dist.all_gather(parts, send, group=group)
+        out = torch.cat(parts, 0)
+    else:
+        dist.all_gather_into_tensor(out, send, group=group)
+    if n_total % world == 0:
+        return out
+    keep = []
+    for r in range(world):
+        a, b = shard_bounds(n_total, r, world)
+        keep.append(out[r * cap: r * cap + (b - a)])
+    return torch.cat(keep, 0)
+
+
+class ShardedSegmenter:
+    """Runs ``segment_fn`` (e.g. ``lambda x: model.forward_masks(x, packed=True)``) on this
+    rank's shard of a global batch and all-gathers the masks to every rank."""
+
+    def __init__(self, segment_fn, group=None):
+        self.segment_fn = segment_fn
+        self.group = group
+
+    def __call__(self, x_global_or_local: torch.Tensor, n_total: int | None = None,
+                 already_local: bool = False) -> torch.Tensor:
+        world = dist.get_world_size(self.group)
+        rank = dist.get_rank(self.group)
+        if already_local:
+            if n_total is None:
+                raise ValueError("n_total is required with already_local=True")
+            local = x_global_or_local
+        else:
+            n_total = x_global_or_local.shape[0]
+            lo, hi = shard_bounds(n_total, rank, world)
+            local = x_global_or_local[lo:hi]
+        masks = self.segment_fn(local)
+        return all_gather_rows(masks, n_total, self.group)

@@ -15,7 +15,7 @@ import numpy as np
 import torch  # noqa: F401  (must precede the library load, see module docstring)
 
 LIB_NAME = "libunet_mi355x.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("UNET_MI355X_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 UNET_OK, UNET_EINVAL, UNET_ESHAPE, UNET_ENOMEM, UNET_EHIP, UNET_ESTATE, UNET_EKEY = 0, -1, -2, -3, -4, -5, -6
 DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16": 2}
@@ -43,6 +43,7 @@ SIGNATURES = {
     "unet_reserve": (_i, [_vp, _i, _i, _i]),
     "unet_forward": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp]),
     "unet_num_launches": (_i, []),
+    "unet_launch_label": (ctypes.c_char_p, [_vp, _i]),
     "unet_forward_timed": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
     "unet_debug_fetch": (_i, [_vp, ctypes.c_char_p, _vp, ctypes.POINTER(_sz), _vp]),
     "unet_destroy": (_i, [_vp]),
@@ -149,6 +150,10 @@ class Handle:
                                               None if masks is None else masks.data_ptr(),
                                               mask_kind, n, h, w, stream, ms), "unet_forward_timed")
         return list(ms)
+
+    def launch_labels(self) -> list:
+        """Kernel instantiation of every launch of a forward (include/unet_mi355x.h order)."""
+        return [self.lib.unet_launch_label(self._h, i).decode() for i in range(self.lib.unet_num_launches())]
 
     def debug_fetch(self, name: str, stream: int) -> int:
         cnt = ctypes.c_size_t(0)
