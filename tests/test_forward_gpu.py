@@ -170,7 +170,7 @@ def test_weight_update_repacks():
     m.close()
 
 
-@pytest.mark.parametrize("cfg", list(range(16)))
+@pytest.mark.parametrize("cfg", list(range(18)))
 def test_every_kernel_config(cfg, monkeypatch):
     """Each implicit-GEMM configuration (csrc/unet_internal.h Cfg) forced on every 3x3 layer
     it supports, checked against the reference golden (fp32 and bf16)."""

@@ -67,6 +67,8 @@ inline int natural_of_packed(int rho) {
   return g + (r >> 2) * 16 + t * 4 + (r & 3);
 }
 
+bool is_fused_in(int cfg) { return cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8; }
+
 struct Layer {
   int cin = 0, cout = 0, ctot = 0, taps = 9, cfg = CFG_R128_P128;
   void* w = nullptr;   // packed [ctot][taps*cin] element type
@@ -111,18 +113,19 @@ const int kLayerCh[17][2] = {{64, 64},    {64, 128},   {128, 128}, {128, 256}, {
                              {1024, 512}, {512, 512},  {512, 256}, {256, 256},
                              {256, 128},  {128, 128},  {128, 64},  {64, 64}};
 // Default kernel configuration per 3x3 layer, from in-process A/B timing on MI355X at
-// bs256 512x512 bf16 (tools/tune.py; profiles/tune_r1.txt).  Two-blocks-per-CU halo tiles
-// (64 rows) win wherever the pixel grid is large relative to K; the persistent 128-row
-// halo kernel wins on the deep decoder convs.
+// bs256 512x512 bf16 (tools/tune.py; profiles/tune_r1*.txt).  All are two-blocks-per-CU
+// single-halo tiles; 128-row x 64-pixel wave tiles (fewer LDS reads per MFMA) win on the
+// plain-store layers, 64x64 wave tiles on the deeper pooled layers and at 512x512.
 const int kDefaultCfg[17] = {
-    CFG_HALO1_R64_W8,                                       // down1.3 (+pool)
-    CFG_HALO1_R64_W4, CFG_HALO1_R64_W4, CFG_HALO1_R64_W4,    // down2.0 down2.3 down3.0
-    CFG_HALO1_R64_W4, CFG_HALO1_R64_W4, CFG_HALO1_R64_W4,    // down3.3 down4.0 down4.3
-    CFG_HALO1_R64_W4, CFG_HALO1_R64_W4,                      // bottleneck.0 .3
-    CFG_HALO_R128_W8, CFG_HALO_R128_W8,                      // conv4.0 conv4.3
-    CFG_HALO1_R64_W4, CFG_HALO_R128_W8,                      // conv3.0 conv3.3
-    CFG_HALO1_R64_W4, CFG_HALO_R128_W8,                      // conv2.0 conv2.3
-    CFG_HALO1_R64_W4, CFG_HALO1_R64_W8};                     // conv1.0, conv1.3 (+head)
+    CFG_FUSED_IN_W8,                                             // down1.0 + down1.3 (+pool), fused
+    CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // down2.0, down2.3 (+pool)
+    CFG_HALO1_R128T8_NS2, CFG_HALO1_R64_W4,                      // down3.0, down3.3 (+pool)
+    CFG_HALO1_R128T8_NS2, CFG_HALO1_R64_W4,                      // down4.0, down4.3 (+pool)
+    CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // bottleneck.0 .3
+    CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // conv4.0 conv4.3
+    CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // conv3.0 conv3.3
+    CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // conv2.0 conv2.3
+    CFG_HALO1_R64_W4, CFG_HALO1_R64_W8};                         // conv1.0, conv1.3 (+head)                     // conv1.0, conv1.3 (+head)
 const char* kUpKey[4] = {"up4", "up3", "up2", "up1"};
 const int kUpCh[4][2] = {{1024, 512}, {512, 256}, {256, 128}, {128, 64}};
 
@@ -275,13 +278,14 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
   struct { int wr, wpx, tc, hb, ns, pipe; } halo[] = {
       {2, 2, 4, 2, 3, 0}, {2, 4, 4, 2, 3, 0}, {1, 4, 4, 2, 3, 0}, {1, 8, 4, 2, 3, 0}, {1, 4, 4, 1, 3, 0},
       {1, 8, 4, 1, 3, 0}, {2, 2, 4, 1, 2, 0}, {2, 4, 4, 2, 3, 1}, {1, 4, 4, 1, 3, 1}, {1, 8, 4, 1, 3, 1},
-      {1, 4, 8, 1, 2, 0}, {1, 4, 8, 1, 3, 0}};
+      {1, 4, 8, 1, 2, 0}, {1, 4, 8, 1, 3, 0}, {1, 4, 4, 1, 3, 0}, {1, 8, 4, 1, 3, 0}};
   if (cfg >= CFG_COUNT) {
     std::snprintf(buf, sizeof buf, "ablation_%d<%s, %d>", cfg - CFG_COUNT, tname(t), epi);
   } else if (cfg_is_halo(cfg)) {
     const auto& c = halo[cfg - CFG_HALO_R128_W4];
-    std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, %d, %d, %d, %d, %d, %d, %d>", tname(t), c.wr, c.wpx,
-                  c.tc, c.hb, c.ns, c.pipe, epi);
+    const int hsrc = (cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8) ? 1 : 0;
+    std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, %d, %d, %d, %d, %d, %d, %d, %d>", tname(t), c.wr, c.wpx,
+                  c.tc, c.hb, c.ns, c.pipe, hsrc, epi);
   } else {
     const int wr = cfg_rows(cfg) / 64, wpx = 4 / wr, tp = cfg_pixels(cfg) / (16 * wpx);
     std::snprintf(buf, sizeof buf, "igemm_kernel<%s, %d, %d, %d, %d, %d>", tname(t), wr, wpx, tp, taps, epi);
@@ -299,7 +303,7 @@ void build_labels(unet_handle* h) {
                                         101, C3A, C3B, 102, C2A, C2B, 103, C1A, C1B};
   for (int i = 0; i < UNET_NUM_LAUNCHES; ++i) {
     const int id = order[i];
-    if (id < 0) { h->labels[i] = buf; continue; }
+    if (id < 0) { h->labels[i] = is_fused_in(h->L[D1B].cfg) ? "fused_into_down1.3" : buf; continue; }
     if (id >= 100) { h->labels[i] = layer_label(h->dt, h->U[id - 100].cfg, 1, EPI_UPSCATTER); continue; }
     const int epi = id == C1B ? EPI_HEAD : (id == D1B || id == D2B || id == D3B || id == D4B) ? EPI_POOL : EPI_STORE;
     h->labels[i] = layer_label(h->dt, h->L[id].cfg, 9, epi);
@@ -358,6 +362,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   }
   for (int i = 0; i < 17; ++i) {   // keep every layer on a configuration it supports
     Layer& L = h->L[i];
+    const bool fused_in = L.cfg == CFG_FUSED_IN_W4 || L.cfg == CFG_FUSED_IN_W8;
+    if (fused_in && (i != D1B || cfg->dtype == UNET_DTYPE_F32)) L.cfg = L.cout == 64 ? CFG_HALO1_R64_W8 : CFG_R128_P128;
     if (cfg_rows(L.cfg) > L.cout || L.cfg == CFG_R128_P256 || (cfg_single_chunk(L.cfg) && L.cin != chunk))
       L.cfg = L.cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
     if (i == C1B && cfg_rows(L.cfg) != 64) L.cfg = CFG_R64_P128;
@@ -473,7 +479,8 @@ namespace {
 
 int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, int H, int W, int ldi,
               void* out, int ldo, int out_off, void* out2, int ldo2, hipStream_t s,
-              float* logits = nullptr, void* masks = nullptr, int mask_kind = MASK_NONE) {
+              float* logits = nullptr, void* masks = nullptr, int mask_kind = MASK_NONE,
+              const float* x0 = nullptr) {
   IgemmArgs a{};
   a.in = in;
   a.wgt = L.w;
@@ -491,6 +498,12 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.ldo = ldo; a.out_off = out_off; a.ldo2 = ldo2;
   a.ncls = h->cfg.n_classes;
   a.mask_kind = mask_kind;
+  if (is_fused_in(L.cfg)) {
+    a.x0 = x0;
+    a.w0p = h->w0p;
+    a.b0 = h->b0;
+    a.c0 = h->cfg.n_channels;
+  }
   for (int i = 0; i < kMaxClasses; ++i) a.thr[i] = h->cfg.thresholds[i];
   const int BR = cfg_rows(L.cfg), BP = cfg_pixels(L.cfg);
   const int TH = BP / 16;
@@ -540,13 +553,17 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   int li = 0;
   auto mark = [&]() { if (ev) (void)hipEventRecord(ev[li], s); ++li; };
   mark();
-  hipError_t e = launch_first_conv(h->dt, f, s);
-  if (e != hipSuccess) return fail(UNET_EHIP, std::string("first conv launch: ") + hipGetErrorString(e));
+  const bool fused_in = is_fused_in(h->L[D1B].cfg);   // down1.0 computed inside down1.3
+  if (!fused_in) {
+    hipError_t e = launch_first_conv(h->dt, f, s);
+    if (e != hipSuccess) return fail(UNET_EHIP, std::string("first conv launch: ") + hipGetErrorString(e));
+  }
 
 #define RUN(...) do { mark(); rc = run_igemm(__VA_ARGS__); if (rc) return rc; } while (0)
   // encoder: conv b of each level writes the skip into the upper half of the concat
   // buffer (torch.cat([up, skip]) puts skip second, unet_model.py:71) and the pooled map.
-  RUN(h, h->L[D1B], EPI_POOL, buf(B.tA), N, H, W, 64, buf(B.cat1), 128, 64, buf(B.p1), 64, s);
+  RUN(h, h->L[D1B], EPI_POOL, buf(B.tA), N, H, W, 64, buf(B.cat1), 128, 64, buf(B.p1), 64, s,
+      nullptr, nullptr, MASK_NONE, static_cast<const float*>(x));
   RUN(h, h->L[D2A], EPI_STORE, buf(B.p1), N, H2, W2, 64, buf(B.tA), 128, 0, nullptr, 0, s);
   RUN(h, h->L[D2B], EPI_POOL, buf(B.tA), N, H2, W2, 128, buf(B.cat2), 256, 128, buf(B.p2), 128, s);
   RUN(h, h->L[D3A], EPI_STORE, buf(B.p2), N, H4, W4, 128, buf(B.tA), 256, 0, nullptr, 0, s);

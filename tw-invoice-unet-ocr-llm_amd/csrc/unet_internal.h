@@ -46,6 +46,11 @@ struct IgemmArgs {
   int ncls, mask_kind;
   float thr[kMaxClasses];
   int tiles_x, tiles_y, n_ct, n_blocks;
+  // fused first conv (halo computed from the raw input instead of loaded): down1.0 + down1.3
+  const float* x0;     // NCHW fp32 network input [N][c0][H][W]
+  const void* w0p;     // first conv packed [64][32] element type (rows permuted)
+  const float* b0;     // first conv folded bias [64]
+  int c0;              // network input channels (1 or 3)
 };
 
 struct FirstConvArgs {
@@ -70,7 +75,9 @@ enum Cfg : int {
   CFG_PHALO_R128_W8 = 11, CFG_PHALO1_R64_W4 = 12, CFG_PHALO1_R64_W8 = 13,
   // 128-row x 64-pixel wave tiles (4 waves, 128 x 256 block), single halo buffer
   CFG_HALO1_R128T8_NS2 = 14, CFG_HALO1_R128T8_NS3 = 15,
-  CFG_COUNT = 16
+  // down1.3 with down1.0 fused: the 18x18x64 halo is computed from the raw input (16-bit)
+  CFG_FUSED_IN_W4 = 16, CFG_FUSED_IN_W8 = 17,
+  CFG_COUNT = 18
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);

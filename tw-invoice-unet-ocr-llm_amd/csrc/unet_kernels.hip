@@ -394,7 +394,7 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int EPI>
+template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int HSRC, int EPI>
 __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void conv3x3_halo_kernel(const IgemmArgs a) {
   // HB = 2 (persistent): gridDim.x = n_ct * n_slots blocks (host), each with a fixed row
   // tile ct, walks pixel tiles mt = slot, slot + n_slots, ...  The K-step pipeline (halo of
@@ -405,6 +405,9 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   // for two blocks per CU, which then cover each other's halo loads and epilogues.
   // NS = weight-ring slots; weights are prefetched NS-1 steps ahead.
   // TCW = 16-row MFMA tiles per wave (4: 64 rows, 8: 128 rows = two 64-row epilogue groups).
+  // HSRC = 1: the layer is down1.3 and its input (down1.0's output) is never materialised:
+  // the 18x18x64 halo is computed in the prologue from the raw fp32 input (first conv on
+  // MFMA, K = 9*C padded to 32), which removes a 32 MB/image write + read.
   constexpr int NW = WR * WPX;
   constexpr int TC = TCW;
   constexpr int TP = 16 / WPX;
@@ -418,7 +421,10 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   constexpr int WSLOT = BR * 128;
   constexpr int WOFF = HB * HALO_BYTES;
   constexpr int PARAM_OFF = WOFF + NS * WSLOT;
-  __shared__ __attribute__((aligned(16))) char lds[PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4];
+  constexpr int XS_OFF = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
+  constexpr int XS_FLOATS = HSRC ? 3 * 20 * 20 : 0;
+  static_assert(HSRC == 0 || (HB == 1 && sizeof(T) == 2), "fused input halo: single buffer, 16-bit");
+  __shared__ __attribute__((aligned(16))) char lds[XS_OFF + XS_FLOATS * 4];
   float* bias_s = reinterpret_cast<float*>(lds + PARAM_OFF);
   float* headw_s = bias_s + BR;
   float* headb_s = headw_s + kMaxClasses * 64;
@@ -517,6 +523,71 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   }
   const int px_lane = col & 7;
 
+  if constexpr (HSRC == 1) {
+    issue_w(0);
+    if (NS == 3 && total > 1) issue_w(1);
+    // --- fused down1.0: raw input window 20x20xC -> first conv on MFMA -> LDS halo ---
+    float* xs = reinterpret_cast<float*>(lds + XS_OFF);
+    int n0, ty0, tx0;
+    tile_of(0, n0, ty0, tx0);
+    const int C0 = a.c0;
+    for (int i = tid; i < C0 * 400; i += 64 * NW) {
+      const int c = i / 400, r = i - c * 400, yy = r / 20, xx = r - (r / 20) * 20;
+      const int iy = ty0 * 16 + yy - 2, ix = tx0 * 16 + xx - 2;
+      const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      xs[i] = ok ? a.x0[(((long long)n0 * C0 + c) * H + iy) * W + ix] : 0.f;
+    }
+    frag_t wf[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      wf[t] = *reinterpret_cast<const frag_t*>(reinterpret_cast<const char*>(a.w0p) +
+                                               ((t * 16 + (lane & 15)) * 32 + 8 * (lane >> 4)) * sizeof(T));
+    float b0v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) b0v[e] = a.b0[(lane >> 4) * 16 + e];
+    int koff[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * (lane >> 4) + j;
+      const int c = k / 9, r = k - (k / 9) * 9;
+      koff[j] = k < 9 * C0 ? c * 400 + (r / 3) * 20 + (r - (r / 3) * 3) : -1;
+    }
+    __syncthreads();
+    for (int grp = wave; grp * 16 < kHaloPix; grp += NW) {
+      const int p = grp * 16 + (lane & 15);
+      const bool real = p < kHaloPix;
+      const int hy = real ? p / 18 : 0, hx = real ? p - (p / 18) * 18 : 0;
+      typedef T t8 __attribute__((ext_vector_type(8)));
+      t8 hv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hv[j] = (T)(koff[j] >= 0 ? xs[koff[j] + hy * 20 + hx] : 0.f);
+      const uint4 bfr = __builtin_bit_cast(uint4, hv);
+      f32x4 acc0[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mfma_frag<T>(acc0[t], __builtin_bit_cast(uint4, wf[t]), bfr);
+      }
+      // zero outside the image: these are down1.3's conv padding, not relu(bias)
+      const int iy = ty0 * 16 + hy - 1, ix = tx0 * 16 + hx - 1;
+      const bool inimg = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      t8 lo, hi;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = inimg ? fmaxf(acc0[t][e] + b0v[t * 4 + e], 0.f) : 0.f;
+          if (t < 2) lo[t * 4 + e] = (T)v; else hi[(t - 2) * 4 + e] = (T)v;
+        }
+      if (real) {
+        const int q = lane >> 4;
+        char* row = lds + p * 128;
+        *reinterpret_cast<uint4*>(row + (((2 * q) ^ (hx & 7)) << 4)) = __builtin_bit_cast(uint4, lo);
+        *reinterpret_cast<uint4*>(row + (((2 * q + 1) ^ (hx & 7)) << 4)) = __builtin_bit_cast(uint4, hi);
+      }
+    }
+    if (NS == 3 && total > 1) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
+  } else {
   issue_halo(0);
   issue_w(0);
   if (NS == 3 && total > 1) {
@@ -524,6 +595,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     wait_vm_barrier<WI>();
   } else {
     wait_vm_barrier<0>();
+  }
   }
 
   // fragment reads of (step, kk) into a register set
@@ -578,6 +650,8 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     } else {
       read_frags(g, hseq, tap, 0, a0, b0);
       mfmas(a0, b0);
+      // 128-row wave tiles: keep one kk's fragments live at a time (register budget)
+      if constexpr (TC == 8) __builtin_amdgcn_sched_barrier(0);
       read_frags(g, hseq, tap, 1, a1, b1);
       mfmas(a1, b1);
     }
@@ -749,7 +823,7 @@ static hipError_t launch_one(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int EPI>
+template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int EPI, int HSRC = 0>
 static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   // HB=2: persistent grid, n_ct row tiles x n_slots pixel-tile walkers, ~one block per CU.
   // HB=1: one block per (row tile, pixel tile), two blocks per CU.
@@ -760,7 +834,8 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
     if (n_slots < 1) n_slots = 1;
     if (n_slots > n_mt) n_slots = n_mt;
   }
-  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, HB, NS, PIPE, EPI>), dim3(a.n_ct * n_slots),
+  if (HSRC && (a.Cin != Elem<T>::BKE || a.c0 < 1 || a.c0 > 3 || !a.x0 || !a.w0p)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, HB, NS, PIPE, HSRC, EPI>), dim3(a.n_ct * n_slots),
                      dim3(64 * WR * WPX), 0, s, a);
   return hipGetLastError();
 }
@@ -781,6 +856,13 @@ static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
       case CFG_PHALO1_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 1, EPI>(a, s);
       case CFG_HALO1_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 0, EPI>(a, s);
       case CFG_HALO1_R128T8_NS3: return launch_halo<T, 1, 4, 8, 1, 3, 0, EPI>(a, s);
+      case CFG_FUSED_IN_W4:
+      case CFG_FUSED_IN_W8:
+        if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) {
+          if (cfg == CFG_FUSED_IN_W4) return launch_halo<T, 1, 4, 4, 1, 3, 0, EPI, 1>(a, s);
+          return launch_halo<T, 1, 8, 4, 1, 3, 0, EPI, 1>(a, s);
+        }
+        return hipErrorInvalidValue;
 #ifdef UNET_ABLATION   // timing-only builds: wrong outputs by construction
       case CFG_COUNT + 0: return launch_halo<T, 1, 4, 4, 1, 3, 2, EPI>(a, s);   // HALO1_R64_W4, no MFMA
       case CFG_COUNT + 1: return launch_halo<T, 1, 4, 4, 1, 3, 3, EPI>(a, s);   // HALO1_R64_W4, no DMA
