@@ -170,7 +170,7 @@ def test_weight_update_repacks():
     m.close()
 
 
-@pytest.mark.parametrize("cfg", list(range(18)))
+@pytest.mark.parametrize("cfg", list(range(23)))
 def test_every_kernel_config(cfg, monkeypatch):
     """Each implicit-GEMM configuration (csrc/unet_internal.h Cfg) forced on every 3x3 layer
     it supports, checked against the reference golden (fp32 and bf16)."""
@@ -184,4 +184,22 @@ def test_every_kernel_config(cfg, monkeypatch):
         err = rel_err(out, z["logits"])
         print(f"cfg {cfg} {dtype}: rel err {err:.3e}")
         assert err <= TOL[dtype]
+        m.close()
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 5, 8, 9, 14])
+def test_convtranspose_configs(cfg, monkeypatch):
+    """ConvTranspose2d (up4..up1) on every supported kernel configuration vs the golden."""
+    monkeypatch.setenv("UNET_MI355X_UPCFG", ",".join(f"{i}:{cfg}" for i in range(4)))
+    z = np.load(os.path.join(GOLD, "unet_c3_h16w16_n3_structured.npz"))
+    sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile=str(z["profile"]))
+    for dtype in ("fp32", "bf16"):
+        m = make_model(sd, 3, dtype)
+        with torch.no_grad():
+            out = m(torch.from_numpy(z["x"]).to(DEV)).cpu().numpy()
+        for name, key in (("u1", "inter_u1_up"), ("u4", "inter_u4_up")):
+            ref = z[key]
+            got = m.intermediate(name).cpu().numpy().reshape(ref.shape)
+            assert rel_err(got, ref) <= TOL[dtype], (cfg, dtype, name)
+        assert rel_err(out, z["logits"]) <= TOL[dtype]
         m.close()

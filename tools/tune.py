@@ -2,8 +2,8 @@
 
     python tools/tune.py --dtype bf16 --batch 256 --cands "0:2,15:2,16:1" "0:9,16:9" ...
 
-Each candidate is a UNET_MI355X_CFG override string (layer index into the 17 implicit-GEMM
-3x3 layers : Cfg enum value, see csrc/unet_internal.h).  Prints per-launch ms (median of
+Each candidate is "<UNET_MI355X_CFG>|<UNET_MI355X_UPCFG>": layer index into the 17 3x3 layers
+(or 0..3 = up4..up1 after the '|') : Cfg enum value, see csrc/unet_internal.h.  Prints per-launch ms (median of
 --reps timed forwards) for every candidate, interleaved round-robin.
 """
 import argparse
@@ -37,7 +37,9 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     handles = []
     for c in a.cands:
-        os.environ["UNET_MI355X_CFG"] = c
+        lc, _, uc = c.partition("|")        # "<3x3 layer overrides>|<up overrides>"
+        os.environ["UNET_MI355X_CFG"] = lc
+        os.environ["UNET_MI355X_UPCFG"] = uc
         m = UNet(3, 3, compute_dtype=a.dtype)
         m.load_state_dict(sd)
         m = m.to(dev).eval()

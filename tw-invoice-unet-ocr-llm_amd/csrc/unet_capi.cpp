@@ -126,6 +126,7 @@ const int kDefaultCfg[17] = {
     CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // conv3.0 conv3.3
     CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // conv2.0 conv2.3
     CFG_HALO1_R64_W4, CFG_HALO1_R64_W8};                         // conv1.0, conv1.3 (+head)                     // conv1.0, conv1.3 (+head)
+const int kDefaultUpCfg[4] = {CFG_HALO1_R128T8_NS2, CFG_HALO_R128_W8, CFG_HALO_R128_W8, CFG_HALO_R128_W8};  // up4..up1
 const char* kUpKey[4] = {"up4", "up3", "up2", "up1"};
 const int kUpCh[4][2] = {{1024, 512}, {512, 256}, {256, 128}, {128, 64}};
 
@@ -278,14 +279,15 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
   struct { int wr, wpx, tc, hb, ns, pipe; } halo[] = {
       {2, 2, 4, 2, 3, 0}, {2, 4, 4, 2, 3, 0}, {1, 4, 4, 2, 3, 0}, {1, 8, 4, 2, 3, 0}, {1, 4, 4, 1, 3, 0},
       {1, 8, 4, 1, 3, 0}, {2, 2, 4, 1, 2, 0}, {2, 4, 4, 2, 3, 1}, {1, 4, 4, 1, 3, 1}, {1, 8, 4, 1, 3, 1},
-      {1, 4, 8, 1, 2, 0}, {1, 4, 8, 1, 3, 0}, {1, 4, 4, 1, 3, 0}, {1, 8, 4, 1, 3, 0}};
+      {1, 4, 8, 1, 2, 0}, {1, 4, 8, 1, 3, 0}, {1, 4, 4, 1, 3, 0}, {1, 8, 4, 1, 3, 0},
+      {1, 4, 4, 1, 3, 0}, {1, 4, 4, 2, 3, 0}, {1, 2, 4, 2, 3, 0}, {1, 8, 4, 3, 3, 0}, {1, 4, 4, 3, 3, 0}};
   if (cfg >= CFG_COUNT) {
     std::snprintf(buf, sizeof buf, "ablation_%d<%s, %d>", cfg - CFG_COUNT, tname(t), epi);
   } else if (cfg_is_halo(cfg)) {
     const auto& c = halo[cfg - CFG_HALO_R128_W4];
     const int hsrc = (cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8) ? 1 : 0;
-    std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, %d, %d, %d, %d, %d, %d, %d, %d>", tname(t), c.wr, c.wpx,
-                  c.tc, c.hb, c.ns, c.pipe, hsrc, epi);
+    std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d>", tname(t), c.wr,
+                  c.wpx, c.tc, c.hb, c.ns, c.pipe, hsrc, taps == 9 ? 3 : 1, cfg_pixels(cfg) / 16, epi);
   } else {
     const int wr = cfg_rows(cfg) / 64, wpx = 4 / wr, tp = cfg_pixels(cfg) / (16 * wpx);
     std::snprintf(buf, sizeof buf, "igemm_kernel<%s, %d, %d, %d, %d, %d>", tname(t), wr, wpx, tp, taps, epi);
@@ -374,7 +376,24 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     h->U[i].cout = kUpCh[i][1];
     h->U[i].ctot = 4 * kUpCh[i][1];
     h->U[i].taps = 1;
-    h->U[i].cfg = CFG_R128_P128;
+    h->U[i].cfg = ps == "gather" ? CFG_R128_P128 : kDefaultUpCfg[i];
+  }
+  if (const char* ov = std::getenv("UNET_MI355X_UPCFG")) {   // "i:cfg,..." i = 0..3 (up4..up1)
+    std::string o(ov);
+    size_t pos = 0;
+    while (pos < o.size()) {
+      size_t end = o.find(',', pos);
+      if (end == std::string::npos) end = o.size();
+      const std::string item = o.substr(pos, end - pos);
+      const size_t colon = item.find(':');
+      if (colon != std::string::npos) {
+        const int li = std::atoi(item.substr(0, colon).c_str()), c = std::atoi(item.substr(colon + 1).c_str());
+        if (li >= 0 && li < 4 && (c == CFG_R128_P128 || c == CFG_R64_P128 || c == CFG_HALO1_R64_W4 ||
+                                  c == CFG_HALO1_R128T8_NS2 || c == CFG_HALO_R128_W8 || c == CFG_HALO1_R64_W8))
+          h->U[li].cfg = c;
+      }
+      pos = end + 1;
+    }
   }
   DeviceGuard g(cfg->device);
   std::vector<uint8_t> z(256, 0);
@@ -513,8 +532,34 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   const long long nb = (long long)N * a.tiles_x * a.tiles_y * a.n_ct;
   if (nb <= 0 || nb > 0x7FFFFFFFLL) return fail(UNET_ESHAPE, "grid too large");
   a.n_blocks = (int)nb;
+#ifdef UNET_ABLATION
+  // diagnostic build: stamped configurations report a per-wave cycle breakdown on stderr
+  static unsigned long long* dbg = nullptr;
+  const bool stamped = L.cfg >= CFG_COUNT + 7 && L.cfg <= CFG_COUNT + 10;
+  const size_t dbg_n = (size_t)16 * 1024 * 1024;
+  if (stamped && !dbg) (void)hipMalloc((void**)&dbg, dbg_n * 8);
+  if (stamped && dbg) {
+    (void)hipMemsetAsync(dbg, 0, dbg_n * 8, s);
+    a.dbg = dbg;
+  }
+#endif
   hipError_t e = launch_igemm(h->dt, L.cfg, L.taps, epi, a, s);
   if (e != hipSuccess) return fail(UNET_EHIP, std::string("igemm launch: ") + hipGetErrorString(e));
+#ifdef UNET_ABLATION
+  if (stamped && dbg) {
+    (void)hipStreamSynchronize(s);
+    std::vector<unsigned long long> hbuf(dbg_n);
+    (void)hipMemcpy(hbuf.data(), dbg, dbg_n * 8, hipMemcpyDeviceToHost);
+    double sum[6] = {0, 0, 0, 0, 0, 0};
+    size_t cnt = 0;
+    for (size_t i = 0; i + 8 <= dbg_n; i += 8)
+      if (hbuf[i + 6]) { for (int k = 0; k < 6; ++k) sum[k] += (double)hbuf[i + k]; ++cnt; }
+    if (cnt)
+      std::fprintf(stderr, "[stamp] cfg %d Cin %d Cout %d HxW %dx%d waves %zu: avg cycles/wave prologue %.0f "
+                   "compute %.0f wait %.0f epilogue %.0f total %.0f steps %.1f\n", L.cfg, L.cin, L.cout, H, W, cnt,
+                   sum[0] / cnt, sum[1] / cnt, sum[2] / cnt, sum[3] / cnt, sum[4] / cnt, sum[5] / cnt);
+  }
+#endif
   return UNET_OK;
 }
 

@@ -51,6 +51,7 @@ struct IgemmArgs {
   const void* w0p;     // first conv packed [64][32] element type (rows permuted)
   const float* b0;     // first conv folded bias [64]
   int c0;              // network input channels (1 or 3)
+  unsigned long long* dbg;   // diagnostic (ablation build) per-wave cycle stamps, or nullptr
 };
 
 struct FirstConvArgs {
@@ -77,7 +78,11 @@ enum Cfg : int {
   CFG_HALO1_R128T8_NS2 = 14, CFG_HALO1_R128T8_NS3 = 15,
   // down1.3 with down1.0 fused: the 18x18x64 halo is computed from the raw input (16-bit)
   CFG_FUSED_IN_W4 = 16, CFG_FUSED_IN_W8 = 17,
-  CFG_COUNT = 18
+  // 8x16 pixel tiles (10x18 halo, 23 KB): HB=1 -> 3 blocks per CU; HB=2 persistent -> 2 per CU
+  CFG_T8_HALO1_R64_W4 = 18, CFG_T8_HALO_R64_W4 = 19, CFG_T8_HALO_R64_W2 = 20,
+  // persistent, 3-deep halo ring (two chunks / tiles of HBM loads in flight per CU)
+  CFG_HALO3_R64_W8 = 21, CFG_HALO3_R64_W4 = 22,
+  CFG_COUNT = 23
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);

@@ -31,18 +31,21 @@ typedef int frag_t __attribute__((ext_vector_type(4)));   // one 16-byte MFMA op
 
 int cfg_rows(int cfg) {
 #ifdef UNET_ABLATION
-  if (cfg >= CFG_COUNT) return (cfg == CFG_COUNT + 2 || cfg == CFG_COUNT + 3) ? 128 : 64;
+  if (cfg >= CFG_COUNT) return (cfg == CFG_COUNT + 2 || cfg == CFG_COUNT + 3 || cfg == CFG_COUNT + 9) ? 128 : 64;
 #endif
   return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8 ||
           cfg == CFG_HALO1_R128_W4 || cfg == CFG_PHALO_R128_W8 || cfg == CFG_HALO1_R128T8_NS2 ||
           cfg == CFG_HALO1_R128T8_NS3) ? 128 : 64;
 }
 bool cfg_single_chunk(int cfg) { (void)cfg; return false; }
-int cfg_pixels(int cfg) { return (cfg == CFG_R64_P128 || cfg == CFG_R128_P128) ? 128 : 256; }
+int cfg_pixels(int cfg) {
+  return (cfg == CFG_R64_P128 || cfg == CFG_R128_P128 || cfg == CFG_T8_HALO1_R64_W4 || cfg == CFG_T8_HALO_R64_W4 ||
+          cfg == CFG_T8_HALO_R64_W2) ? 128 : 256;
+}
 bool cfg_is_halo(int cfg) { return cfg >= CFG_HALO_R128_W4; }
 int cfg_limit() {
 #ifdef UNET_ABLATION
-  return CFG_COUNT + 7;
+  return CFG_COUNT + 11;
 #else
   return CFG_COUNT;
 #endif
@@ -380,7 +383,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IgemmArgs a) {
 // (128 B), 16-byte chunk c stored at c ^ (hx & 7): conflict-free ds_read_b128 for every tap
 // (the 18-pixel row stride breaks the usual row&7 swizzle).  Weight rows: c ^ (row & 7).
 constexpr int kHaloPix = 18 * 18;
-constexpr int kPersistBlocks = 256;   // one resident block per CU (LDS-limited)
+constexpr int kNumCUs = 256;          // MI355X: 8 XCDs x 32 CUs
 
 // s_waitcnt vmcnt(N) lgkmcnt(0) + s_barrier.  The wait goes through the builtin (not asm) so
 // hipcc's waitcnt tracker knows every LDS read is retired here and does not re-wait for
@@ -394,7 +397,37 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int HSRC, int EPI>
+// Derived geometry / LDS budget of a halo-kernel instantiation (shared with the launcher).
+template <typename T, int WR, int WPX, int TCW, int HB, int NS, int HSRC, int KT, int TH>
+struct HaloGeom {
+  static constexpr int NW = WR * WPX;
+  static constexpr int TC = TCW;
+  static constexpr int TP = TH / WPX;               // 16-pixel groups per wave (TH groups/tile)
+  static constexpr int BR = WR * 16 * TC;
+  static constexpr int BKE = Elem<T>::BKE;
+  static constexpr int PAD = KT == 3 ? 1 : 0;
+  static constexpr int HWD = 16 + 2 * PAD;          // halo width
+  static constexpr int HHT = TH + 2 * PAD;          // halo height
+  static constexpr int NPIX = HWD * HHT;
+  static constexpr int NTAP = KT * KT;
+  // halo DMA is issued by the first HLW waves (all waves, except 4 of 8 for a 3-deep ring so
+  // the per-buffer padding stays small): HI instructions (8 pixel rows each) per loader wave
+  static constexpr int HLW = (HB == 3 && NW > 4) ? 4 : NW;
+  static constexpr int HI = (NPIX + 8 * HLW - 1) / (8 * HLW);
+  static constexpr int HROWS = HI * HLW * 8;
+  static constexpr int WI = BR / (8 * NW);
+  static constexpr int HALO_BYTES = HROWS * 128;
+  static constexpr int WSLOT = BR * 128;
+  static constexpr int WOFF = HB * HALO_BYTES;
+  static constexpr int PARAM_OFF = WOFF + NS * WSLOT;
+  static constexpr int XS_OFF = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
+  static constexpr int XSW = 20, XSH = TH + 4;       // fused input window (HSRC = 1)
+  static constexpr int XS_FLOATS = HSRC ? 3 * XSW * XSH : 0;
+  static constexpr int LDS_BYTES = XS_OFF + XS_FLOATS * 4;
+  static constexpr int BLOCKS_PER_CU = (160 * 1024) / LDS_BYTES;
+};
+
+template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int HSRC, int KT, int TH, int EPI>
 __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void conv3x3_halo_kernel(const IgemmArgs a) {
   // HB = 2 (persistent): gridDim.x = n_ct * n_slots blocks (host), each with a fixed row
   // tile ct, walks pixel tiles mt = slot, slot + n_slots, ...  The K-step pipeline (halo of
@@ -408,23 +441,19 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   // HSRC = 1: the layer is down1.3 and its input (down1.0's output) is never materialised:
   // the 18x18x64 halo is computed in the prologue from the raw fp32 input (first conv on
   // MFMA, K = 9*C padded to 32), which removes a 32 MB/image write + read.
-  constexpr int NW = WR * WPX;
-  constexpr int TC = TCW;
-  constexpr int TP = 16 / WPX;
-  constexpr int BR = WR * 16 * TC;
-  constexpr int BKE = Elem<T>::BKE;
-  constexpr int HI = (kHaloPix + 8 * NW - 1) / (8 * NW);
-  constexpr int HROWS = HI * NW * 8;
-  constexpr int WI = BR / (8 * NW);
+  // KT = 3: 3x3 conv ((TH+2)x18 halo, 9 taps); KT = 1: the same pipeline as a plain GEMM over a
+  // THx16 pixel tile (ConvTranspose2d k2 s2: K = Cin, rows = (a, b, cout), EPI_UPSCATTER).
+  // TH = pixel-tile height (16, or 8 for a smaller LDS footprint and more blocks per CU).
+  using G = HaloGeom<T, WR, WPX, TCW, HB, NS, HSRC, KT, TH>;
+  constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
+  constexpr int HWD = G::HWD, NPIX = G::NPIX, NTAP = G::NTAP, PAD = G::PAD;
+  constexpr int HI = G::HI, WI = G::WI, HALO_BYTES = G::HALO_BYTES, WSLOT = G::WSLOT, HLW = G::HLW;
+  constexpr int WOFF = G::WOFF, PARAM_OFF = G::PARAM_OFF, XS_OFF = G::XS_OFF;
+  constexpr int XSW = G::XSW, XSH = G::XSH;
+  static_assert(TP >= 1 && TH % WPX == 0, "pixel groups per wave");
   static_assert(WI >= 1 && BR % (8 * NW) == 0, "weight tile split");
-  constexpr int HALO_BYTES = HROWS * 128;
-  constexpr int WSLOT = BR * 128;
-  constexpr int WOFF = HB * HALO_BYTES;
-  constexpr int PARAM_OFF = WOFF + NS * WSLOT;
-  constexpr int XS_OFF = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
-  constexpr int XS_FLOATS = HSRC ? 3 * 20 * 20 : 0;
-  static_assert(HSRC == 0 || (HB == 1 && sizeof(T) == 2), "fused input halo: single buffer, 16-bit");
-  __shared__ __attribute__((aligned(16))) char lds[XS_OFF + XS_FLOATS * 4];
+  static_assert(HSRC == 0 || (HB == 1 && sizeof(T) == 2 && KT == 3), "fused input halo: 3x3, single buffer, 16-bit");
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
   float* bias_s = reinterpret_cast<float*>(lds + PARAM_OFF);
   float* headw_s = bias_s + BR;
   float* headb_s = headw_s + kMaxClasses * 64;
@@ -434,6 +463,14 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   const int lane = tid & 63;
   const int wr = wave / WPX;
   const int wp = wave % WPX;
+  // PIPE 6 (diagnostic build only): s_memtime stamps -> per-wave cycle breakdown in a.dbg
+  constexpr bool kStamp = PIPE == 6;
+  auto stamp = [&]() -> unsigned long long {
+    unsigned long long t = 0;
+    if constexpr (kStamp) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+    return t;
+  };
+  unsigned long long st_t0 = stamp(), st_pro = 0, st_cmp = 0, st_wait = 0, st_epi = 0, st_steps = 0;
 
   int bid;
   {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one pixel tile
@@ -449,9 +486,9 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   const int items = (n_mt - slot + n_slots - 1) / n_slots;
 
   const int H = a.H, W = a.W;
-  const int K = 9 * a.Cin;
+  const int K = NTAP * a.Cin;
   const int nch = a.Cin / BKE;
-  const int S = 9 * nch;
+  const int S = NTAP * nch;
   const int total = items * S;
   const int hseq_end = items * nch;
 
@@ -483,24 +520,25 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     const int i = hseq / nch, c = hseq - (hseq / nch) * nch;
     int n, ty, tx;
     tile_of(i, n, ty, tx);
-    char* dst = lds + (HB == 2 ? (hseq & 1) * HALO_BYTES : 0) + wave * HI * 8 * 128;
+    if (wave >= HLW) return;   // (wave-uniform) not a halo loader
+    char* dst = lds + (hseq % HB) * HALO_BYTES + wave * HI * 8 * 128;
     const long long c0 = (long long)c * BKE;
-    const long long pix0 = (long long)(n * H + ty * 16) * W + tx * 16;
+    const long long pix0 = (long long)(n * H + ty * TH) * W + tx * 16;
 #pragma unroll
     for (int j = 0; j < HI; ++j) {
       const int row = (wave * HI + j) * 8 + (lane >> 3);
-      const int hy = row / 18, hx = row - hy * 18;
-      const int iy = ty * 16 + hy - 1, ix = tx * 16 + hx - 1;
-      const bool ok = row < kHaloPix && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const int hy = row / HWD, hx = row - hy * HWD;
+      const int iy = ty * TH + hy - PAD, ix = tx * 16 + hx - PAD;
+      const bool ok = row < NPIX && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       const int chk = ((lane & 7) ^ (hx & 7)) * 16;
-      const long long pix = pix0 + (long long)(hy - 1) * W + (hx - 1);
+      const long long pix = pix0 + (long long)(hy - PAD) * W + (hx - PAD);
       const char* src = ok ? in + (pix * a.ldi + c0) * (long long)sizeof(T) + chk : zero + chk;
       glds16(src, dst + j * 8 * 128);
     }
   };
   auto issue_w = [&](int g) {
     const int s = g % S;
-    const int c = s / 9, tap = s - (s / 9) * 9;
+    const int c = s / NTAP, tap = s - (s / NTAP) * NTAP;
     const size_t koff = ((size_t)tap * a.Cin + (size_t)c * BKE) * sizeof(T);
     char* dst = lds + WOFF + (g % NS) * WSLOT + wave * WI * 8 * 128;
 #pragma unroll
@@ -519,7 +557,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   for (int p = 0; p < TP; ++p) {
     int py, px;
     pix_of((wp * TP + p) * 16 + col, py, px);
-    prow[p] = py * 18 + px;
+    prow[p] = py * HWD + px;
   }
   const int px_lane = col & 7;
 
@@ -531,9 +569,9 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     int n0, ty0, tx0;
     tile_of(0, n0, ty0, tx0);
     const int C0 = a.c0;
-    for (int i = tid; i < C0 * 400; i += 64 * NW) {
-      const int c = i / 400, r = i - c * 400, yy = r / 20, xx = r - (r / 20) * 20;
-      const int iy = ty0 * 16 + yy - 2, ix = tx0 * 16 + xx - 2;
+    for (int i = tid; i < C0 * XSW * XSH; i += 64 * NW) {
+      const int c = i / (XSW * XSH), r = i - c * (XSW * XSH), yy = r / XSW, xx = r - (r / XSW) * XSW;
+      const int iy = ty0 * TH + yy - 2, ix = tx0 * 16 + xx - 2;
       const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       xs[i] = ok ? a.x0[(((long long)n0 * C0 + c) * H + iy) * W + ix] : 0.f;
     }
@@ -550,17 +588,17 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     for (int j = 0; j < 8; ++j) {
       const int k = 8 * (lane >> 4) + j;
       const int c = k / 9, r = k - (k / 9) * 9;
-      koff[j] = k < 9 * C0 ? c * 400 + (r / 3) * 20 + (r - (r / 3) * 3) : -1;
+      koff[j] = k < 9 * C0 ? c * (XSW * XSH) + (r / 3) * XSW + (r - (r / 3) * 3) : -1;
     }
     __syncthreads();
-    for (int grp = wave; grp * 16 < kHaloPix; grp += NW) {
+    for (int grp = wave; grp * 16 < NPIX; grp += NW) {
       const int p = grp * 16 + (lane & 15);
-      const bool real = p < kHaloPix;
+      const bool real = p < NPIX;
       const int hy = real ? p / 18 : 0, hx = real ? p - (p / 18) * 18 : 0;
       typedef T t8 __attribute__((ext_vector_type(8)));
       t8 hv;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) hv[j] = (T)(koff[j] >= 0 ? xs[koff[j] + hy * 20 + hx] : 0.f);
+      for (int j = 0; j < 8; ++j) hv[j] = (T)(koff[j] >= 0 ? xs[koff[j] + hy * XSW + hx] : 0.f);
       const uint4 bfr = __builtin_bit_cast(uint4, hv);
       f32x4 acc0[4];
 #pragma unroll
@@ -569,7 +607,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
         mfma_frag<T>(acc0[t], __builtin_bit_cast(uint4, wf[t]), bfr);
       }
       // zero outside the image: these are down1.3's conv padding, not relu(bias)
-      const int iy = ty0 * 16 + hy - 1, ix = tx0 * 16 + hx - 1;
+      const int iy = ty0 * TH + hy - 1, ix = tx0 * 16 + hx - 1;
       const bool inimg = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       t8 lo, hi;
 #pragma unroll
@@ -590,20 +628,25 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   } else {
   issue_halo(0);
   issue_w(0);
+  if (HB == 3 && hseq_end > 1) issue_halo(1);   // 3-deep ring: two chunks ahead from the start
   if (NS == 3 && total > 1) {
     issue_w(1);
-    wait_vm_barrier<WI>();
+    if (HB == 3 && hseq_end > 1) {
+      if (wave < HLW) wait_vm_barrier<HI + WI>(); else wait_vm_barrier<WI>();
+    } else {
+      wait_vm_barrier<WI>();
+    }
   } else {
-    wait_vm_barrier<0>();
+    if (HB == 3 && hseq_end > 1 && wave < HLW) wait_vm_barrier<HI>(); else wait_vm_barrier<0>();
   }
   }
 
   // fragment reads of (step, kk) into a register set
   auto read_frags = [&](int g, int hs, int tp, int kk, frag_t (&af)[TC], frag_t (&bf)[TP]) {
-    const int dy = tp / 3, dx = tp - (tp / 3) * 3;
-    const char* Hs = lds + (HB == 2 ? (hs & 1) * HALO_BYTES : 0);
+    const int dy = tp / KT, dx = tp - (tp / KT) * KT;
+    const char* Hs = lds + (hs % HB) * HALO_BYTES;
     const char* Ws = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 128;
-    const int toff = dy * 18 + dx;
+    const int toff = dy * HWD + dx;
     const int hx7 = (px_lane + dx) & 7;
     const int chunk = kk * 4 + q;
 #pragma unroll
@@ -634,12 +677,15 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   if (PIPE == 1 || PIPE == 5) read_frags(0, 0, 0, 0, a0, b0);
 
   int c = 0, tap = 0, hseq = 0, item = 0;
+  if constexpr (kStamp) st_pro = stamp() - st_t0;
   for (int g = 0; g < total; ++g) {
-    const bool hnext = HB == 2 && (tap == 0) && (hseq + 1 < hseq_end);
+    const unsigned long long st_a = stamp();
+    // ring of HB halo buffers: at a chunk's first tap, prefetch the halo HB-1 chunks ahead
+    const bool hnext = HB >= 2 && (tap == 0) && (hseq + HB - 1 < hseq_end);
     const bool wnext = g + NS - 1 < total;
     constexpr bool kDma = PIPE < 3;       // ablations 3, 4, 5: no DMA in the loop
     constexpr bool kPipe = PIPE == 1 || PIPE == 5;
-    if (kDma && hnext) issue_halo(hseq + 1);
+    if (kDma && hnext) issue_halo(hseq + HB - 1);
     if (kDma && wnext) issue_w(g + NS - 1);
 
     if (kPipe) {
@@ -657,22 +703,29 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     }
     // the next step needs W(g+1) (and, at a chunk end, the next halo, which is older);
     // the barrier's lgkmcnt(0) also retires every fragment read of this step (WAR)
+    const unsigned long long st_b = stamp();
     if (PIPE == 4) {
       // ablation: no barrier
     } else if (NS == 2) {
       wait_vm_barrier<0>();
-    } else if (hnext) {
+    } else if (hnext && wave < HLW) {
       if (wnext) wait_vm_barrier<HI + WI>(); else wait_vm_barrier<HI>();
     } else {
       if (wnext) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
     }
-    if (HB == 1 && tap == 8 && hseq + 1 < hseq_end) {
+    if (HB == 1 && tap == NTAP - 1 && hseq + 1 < hseq_end) {
       if (kDma) issue_halo(hseq + 1);   // every wave has finished reading the halo (barrier above)
       wait_vm_barrier<0>();
     }
 
+    if constexpr (kStamp) {
+      const unsigned long long st_c = stamp();
+      st_cmp += st_b - st_a;
+      st_wait += st_c - st_b;
+      ++st_steps;
+    }
     bool tile_end = false;
-    if (++tap == 9) {
+    if (++tap == NTAP) {
       tap = 0;
       ++hseq;
       if (++c == nch) {
@@ -688,11 +741,12 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
       mfmas(a1, b1);
     }
     if (tile_end) {
+      const unsigned long long st_e = stamp();
       int n, ty, tx;
       tile_of(item, n, ty, tx);
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<T, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
+        conv_epilogue<T, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * TH, tx * 16,
                                   wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h,
                                   headw_s, headb_s);
 #pragma unroll
@@ -700,6 +754,14 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
 #pragma unroll
         for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
       ++item;
+      if constexpr (kStamp) st_epi += stamp() - st_e;
+    }
+  }
+  if constexpr (kStamp) {
+    const unsigned long long tot = stamp() - st_t0;
+    if (lane == 0 && a.dbg) {
+      unsigned long long* d = a.dbg + ((size_t)blockIdx.x * NW + wave) * 8;
+      d[0] = st_pro; d[1] = st_cmp; d[2] = st_wait; d[3] = st_epi; d[4] = tot; d[5] = st_steps; d[6] = 1;
     }
   }
 }
@@ -823,19 +885,22 @@ static hipError_t launch_one(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int EPI, int HSRC = 0>
+template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int EPI, int HSRC = 0, int KT = 3,
+          int TH = 16>
 static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
-  // HB=2: persistent grid, n_ct row tiles x n_slots pixel-tile walkers, ~one block per CU.
-  // HB=1: one block per (row tile, pixel tile), two blocks per CU.
+  // HB=2: persistent grid, n_ct row tiles x n_slots pixel-tile walkers, as many blocks as
+  // fit per CU (LDS-limited).  HB=1: one block per (row tile, pixel tile).
+  using G = HaloGeom<T, WR, WPX, TCW, HB, NS, HSRC, KT, TH>;
+  if (a.tiles_y != (a.H + TH - 1) / TH) return hipErrorInvalidValue;   // host tiling must match
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
   int n_slots = n_mt;
-  if (HB == 2) {
-    n_slots = kPersistBlocks / a.n_ct;
+  if (HB >= 2) {
+    n_slots = (kNumCUs * G::BLOCKS_PER_CU) / a.n_ct;
     if (n_slots < 1) n_slots = 1;
     if (n_slots > n_mt) n_slots = n_mt;
   }
   if (HSRC && (a.Cin != Elem<T>::BKE || a.c0 < 1 || a.c0 > 3 || !a.x0 || !a.w0p)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, HB, NS, PIPE, HSRC, EPI>), dim3(a.n_ct * n_slots),
+  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, HB, NS, PIPE, HSRC, KT, TH, EPI>), dim3(a.n_ct * n_slots),
                      dim3(64 * WR * WPX), 0, s, a);
   return hipGetLastError();
 }
@@ -856,6 +921,11 @@ static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
       case CFG_PHALO1_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 1, EPI>(a, s);
       case CFG_HALO1_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 0, EPI>(a, s);
       case CFG_HALO1_R128T8_NS3: return launch_halo<T, 1, 4, 8, 1, 3, 0, EPI>(a, s);
+      case CFG_T8_HALO1_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 0, EPI, 0, 3, 8>(a, s);
+      case CFG_T8_HALO_R64_W4: return launch_halo<T, 1, 4, 4, 2, 3, 0, EPI, 0, 3, 8>(a, s);
+      case CFG_T8_HALO_R64_W2: return launch_halo<T, 1, 2, 4, 2, 3, 0, EPI, 0, 3, 8>(a, s);
+      case CFG_HALO3_R64_W8: return launch_halo<T, 1, 8, 4, 3, 3, 0, EPI>(a, s);
+      case CFG_HALO3_R64_W4: return launch_halo<T, 1, 4, 4, 3, 3, 0, EPI>(a, s);
       case CFG_FUSED_IN_W4:
       case CFG_FUSED_IN_W8:
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) {
@@ -871,6 +941,10 @@ static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
       case CFG_COUNT + 4: return launch_halo<T, 1, 4, 4, 1, 3, 4, EPI>(a, s);   // HALO1_R64_W4, no DMA, no barrier
       case CFG_COUNT + 5: return launch_halo<T, 1, 4, 4, 1, 3, 5, EPI>(a, s);   // PHALO1_R64_W4, no DMA
       case CFG_COUNT + 6: return launch_halo<T, 1, 4, 4, 1, 3, 1, EPI>(a, s);   // PHALO1_R64_W4 (same binary A/B)
+      case CFG_COUNT + 7: return launch_halo<T, 1, 4, 4, 1, 3, 6, EPI>(a, s);   // stamped HALO1_R64_W4
+      case CFG_COUNT + 8: return launch_halo<T, 1, 8, 4, 1, 3, 6, EPI>(a, s);   // stamped HALO1_R64_W8
+      case CFG_COUNT + 9: return launch_halo<T, 1, 4, 8, 1, 2, 6, EPI>(a, s);   // stamped HALO1_R128T8_NS2
+      case CFG_COUNT + 10: return launch_halo<T, 1, 8, 4, 3, 3, 6, EPI>(a, s);  // stamped HALO3_R64_W8
 #endif
       default: break;
     }
@@ -895,7 +969,15 @@ static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipSt
       default: return hipErrorInvalidValue;
     }
   }
-  if (taps == 1 && epi == EPI_UPSCATTER) return launch_cfg<T, 1, EPI_UPSCATTER>(cfg, a, s);
+  if (taps == 1 && epi == EPI_UPSCATTER) {
+    switch (cfg) {   // ConvTranspose2d on the tile pipeline (no halo, 1 tap)
+      case CFG_HALO1_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
+      case CFG_HALO1_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 0, EPI_UPSCATTER, 0, 1>(a, s);
+      case CFG_HALO_R128_W8: return launch_halo<T, 2, 4, 4, 2, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
+      case CFG_HALO1_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
+      default: return launch_cfg<T, 1, EPI_UPSCATTER>(cfg, a, s);
+    }
+  }
   return hipErrorInvalidValue;
 }
 
