@@ -131,6 +131,12 @@ const char* unet_last_error(void);
 
 int unet_abi_version(void);
 
+/* Logit cut of a probability threshold: for every fp32 logit x,
+ *   (1 / (1 + expf(-x)) > thr)  ==  (x > unet_logit_cut(thr)).
+ * The masks epilogue thresholds logits with it (inference.py:72-78 thresholds
+ * torch.sigmoid(logits)); host-only, no device call. */
+float unet_logit_cut(float thr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -98,6 +98,7 @@ struct unet_handle {
   int lastN = 0, lastH = 0, lastW = 0;
   std::vector<void*> allocs;
   std::string labels[UNET_NUM_LAUNCHES];   // kernel instantiation of every launch
+  float thr_logit[kMaxClasses];           // per-class logit cut, see unet_logit_cut
 };
 
 namespace {
@@ -126,7 +127,8 @@ const int kDefaultCfg[17] = {
     CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // conv3.0 conv3.3
     CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // conv2.0 conv2.3
     CFG_HALO1_R64_W4, CFG_HALO1_R64_W8};                         // conv1.0, conv1.3 (+head)                     // conv1.0, conv1.3 (+head)
-const int kDefaultUpCfg[4] = {CFG_HALO1_R128T8_NS2, CFG_HALO_R128_W8, CFG_HALO_R128_W8, CFG_HALO_R128_W8};  // up4..up1
+const int kDefaultUpCfg[4] = {CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,
+                               CFG_HALO1_R128T8_NS2};  // up4..up1
 const char* kUpKey[4] = {"up4", "up3", "up2", "up1"};
 const int kUpCh[4][2] = {{1024, 512}, {512, 256}, {256, 128}, {128, 64}};
 
@@ -316,6 +318,39 @@ void build_labels(unet_handle* h) {
 extern "C" {
 
 const char* unet_last_error(void) { return g_err.c_str(); }
+
+namespace {
+// fp32 values in a total order as integers (-0 and +0 share a key), so bisection over keys
+// walks every float between -inf and +inf.
+long long float_key(float f) {
+  int32_t i;
+  std::memcpy(&i, &f, 4);
+  return i >= 0 ? (long long)i : (long long)INT32_MIN - (long long)i;
+}
+float key_float(long long k) {
+  const int32_t i = k >= 0 ? (int32_t)k : (int32_t)((long long)INT32_MIN - k);
+  float f;
+  std::memcpy(&f, &i, 4);
+  return f;
+}
+bool sigmoid_above(float x, float thr) { return 1.0f / (1.0f + std::exp(-x)) > thr; }
+}  // namespace
+
+float unet_logit_cut(float thr) {
+  // The reference thresholds probabilities: torch.sigmoid(logits) > thr (inference.py:72-78).
+  // The fp32 sigmoid is monotone non-decreasing in x, so that predicate is exactly
+  // "x > cut" for the largest float cut at which it is still false; the masks kernel
+  // compares logits against the cut and never evaluates exp.
+  const float inf = INFINITY;
+  long long lo = float_key(-inf), hi = float_key(inf);
+  if (sigmoid_above(-inf, thr)) return -inf;        // every logit passes
+  if (!sigmoid_above(inf, thr)) return inf;         // none passes (thr >= 1, or NaN)
+  while (hi - lo > 1) {                              // pred(lo) false, pred(hi) true
+    const long long mid = lo + (hi - lo) / 2;
+    if (sigmoid_above(key_float(mid), thr)) hi = mid; else lo = mid;
+  }
+  return key_float(lo);
+}
 int unet_abi_version(void) { return UNET_ABI_VERSION; }
 
 int unet_create(const unet_config* cfg, unet_handle** out) {
@@ -329,6 +364,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   unet_handle* h = new unet_handle();
   h->cfg = *cfg;
   h->dt = (DType)cfg->dtype;
+  for (int i = 0; i < kMaxClasses; ++i) h->thr_logit[i] = unet_logit_cut(cfg->thresholds[i]);
   // Kernel configuration per layer (tuned on MI355X).  Overrides for
   // tuning / A-B runs: UNET_MI355X_PRESET=gather (first-generation per-tap kernel for
   // every layer) and UNET_MI355X_CFG="layer:cfg,..." (layer = index into L[], cfg = Cfg).
@@ -365,10 +401,14 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   for (int i = 0; i < 17; ++i) {   // keep every layer on a configuration it supports
     Layer& L = h->L[i];
     const bool fused_in = L.cfg == CFG_FUSED_IN_W4 || L.cfg == CFG_FUSED_IN_W8;
-    if (fused_in && (i != D1B || cfg->dtype == UNET_DTYPE_F32)) L.cfg = L.cout == 64 ? CFG_HALO1_R64_W8 : CFG_R128_P128;
+    // fall back within the same kernel family (LDS-halo configurations all accumulate in the
+    // same K order, so they agree bitwise; the gather kernels order K differently)
+    const bool halo = cfg_is_halo(L.cfg);
+    if (fused_in && (i != D1B || cfg->dtype == UNET_DTYPE_F32))
+      L.cfg = L.cout == 64 ? CFG_HALO1_R64_W8 : CFG_HALO1_R128T8_NS2;
     if (cfg_rows(L.cfg) > L.cout || L.cfg == CFG_R128_P256 || (cfg_single_chunk(L.cfg) && L.cin != chunk))
-      L.cfg = L.cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
-    if (i == C1B && cfg_rows(L.cfg) != 64) L.cfg = CFG_R64_P128;
+      L.cfg = L.cout == 64 ? (halo ? CFG_HALO1_R64_W8 : CFG_R64_P256) : (halo ? CFG_HALO1_R128T8_NS2 : CFG_R128_P128);
+    if (i == C1B && cfg_rows(L.cfg) != 64) L.cfg = halo ? CFG_HALO1_R64_W8 : CFG_R64_P128;
   }
   build_labels(h);
   for (int i = 0; i < 4; ++i) {
@@ -389,7 +429,9 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
       if (colon != std::string::npos) {
         const int li = std::atoi(item.substr(0, colon).c_str()), c = std::atoi(item.substr(colon + 1).c_str());
         if (li >= 0 && li < 4 && (c == CFG_R128_P128 || c == CFG_R64_P128 || c == CFG_HALO1_R64_W4 ||
-                                  c == CFG_HALO1_R128T8_NS2 || c == CFG_HALO_R128_W8 || c == CFG_HALO1_R64_W8))
+                                  c == CFG_HALO1_R128T8_NS2 || c == CFG_HALO_R128_W8 || c == CFG_HALO1_R64_W8 ||
+                                  c == CFG_HALO1_R128T8_NS3 || c == CFG_HALO_R128_W4 || c == CFG_HALO3_R64_W8 ||
+                                  c == CFG_HALO3_R64_W4))
           h->U[li].cfg = c;
       }
       pos = end + 1;
@@ -523,7 +565,7 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
     a.b0 = h->b0;
     a.c0 = h->cfg.n_channels;
   }
-  for (int i = 0; i < kMaxClasses; ++i) a.thr[i] = h->cfg.thresholds[i];
+  for (int i = 0; i < kMaxClasses; ++i) a.thr_logit[i] = h->thr_logit[i];
   const int BR = cfg_rows(L.cfg), BP = cfg_pixels(L.cfg);
   const int TH = BP / 16;
   a.tiles_x = (W + 15) / 16;

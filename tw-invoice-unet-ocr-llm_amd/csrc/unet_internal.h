@@ -44,7 +44,7 @@ struct IgemmArgs {
   int Cout;            // convT: channels per (a,b) group
   int ldo, out_off, ldo2;
   int ncls, mask_kind;
-  float thr[kMaxClasses];
+  float thr_logit[kMaxClasses];   // logit cut per class: sigmoid(x) > thr  <=>  x > thr_logit
   int tiles_x, tiles_y, n_ct, n_blocks;
   // fused first conv (halo computed from the raw input instead of loaded): down1.0 + down1.3
   const float* x0;     // NCHW fp32 network input [N][c0][H][W]

@@ -150,6 +150,21 @@ __device__ __forceinline__ void pix_of(int p, int& py, int& px) {
 // rows rbase .. rbase+15 (the weight packing permutes rows so that MFMA row
 // 4*(lane>>4)+e of row-tile t is natural row 16*(lane>>4) + 4*t + e).
 // Pixel p of the wave = group (g0 + p) of the block tile whose origin is (oy0, ox0).
+// Cross-lane helpers on the VALU (gfx950): DPP for intra-row moves, permlane swaps for
+// the lane^16 / lane^32 exchanges.  Both avoid the LDS crossbar that __shfl_xor uses.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float xsum_lane16(float x) {   // x[l] + x[l ^ 16]
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum_lane32(float x) {   // x[l] + x[l ^ 32]
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 template <typename T, int TP, int EPI>
 __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0,
                                               int ox0, int g0, int row0, const float* bias_w,
@@ -193,8 +208,10 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
         float m[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          float o = fmaxf(v[e], __shfl_xor(v[e], 1));
-          m[e] = fmaxf(o, __shfl_xor(o, 8));
+          // 2x2 window partners are lanes ^1 (quad_perm [1,0,3,2]) and ^8 (row_ror:8):
+          // DPP moves instead of ds_bpermute round trips through LDS.
+          const float o = fmaxf(v[e], dpp_f32<0xB1>(v[e]));
+          m[e] = fmaxf(o, dpp_f32<0x128>(o));
         }
         if ((col & 9) == 0 && oy + 1 < H && ox + 1 < W) {
           const int Ho = H >> 1, Wo = W >> 1;
@@ -213,19 +230,31 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
         store16<T>(dst, v);
       }
     } else {  // EPI_HEAD: 1x1 conv 64 -> ncls on the fp32 activations, then masks
-      for (int c = 0; c < a.ncls; ++c) {
-        const float* hw = head_w + c * 64 + q * 16;
-        float sum = 0.f;
+      // All class dots first (independent FMA chains), then the 4 row-quads of the
+      // wave are summed with permlane16/32 swaps (VALU, no LDS round trip).
+      float logit[kMaxClasses];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) sum = fmaf(hw[e], v[e], sum);
-        sum += __shfl_xor(sum, 16);
-        sum += __shfl_xor(sum, 32);
-        const float logit = sum + head_b[c];
+      for (int c = 0; c < kMaxClasses; ++c) {
+        float sum = 0.f;
+        if (c < a.ncls) {
+          const float* hw = head_w + c * 64 + q * 16;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) sum = fmaf(hw[e], v[e], sum);
+          sum = xsum_lane16(sum);
+          sum = xsum_lane32(sum);
+          sum += head_b[c];
+        }
+        logit[c] = sum;
+      }
+#pragma unroll
+      for (int c = 0; c < kMaxClasses; ++c) {
+        if (c >= a.ncls) break;
         const long long pix = ((long long)(n * a.ncls + c) * H + oy) * W + ox;
-        if (a.logits && q == 0 && inside) a.logits[pix] = logit;
+        if (a.logits && q == 0 && inside) a.logits[pix] = logit[c];
         if (a.mask_kind != MASK_NONE) {
-          const float prob = 1.0f / (1.0f + expf(-logit));   // torch.sigmoid, inference.py:72
-          const bool on = prob > a.thr[c];                    // strict '>', inference.py:76-78
+          // sigmoid(logit) > thr (inference.py:72-78, strict '>') == logit > thr_logit[c]:
+          // the host bisects the fp32 sigmoid for the exact logit cut (unet_capi.cpp).
+          const bool on = logit[c] > a.thr_logit[c];
           if (a.mask_kind == MASK_U8) {
             if (q == 0 && inside) a.masks[pix] = on ? 1 : 0;
           } else {
@@ -492,13 +521,16 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   const int total = items * S;
   const int hseq_end = items * nch;
 
-  // per-block parameters into LDS (plain loads, before any DMA is in flight)
-  for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];
-  if (EPI == EPI_HEAD) {
-    for (int i = tid; i < a.ncls * 64; i += 64 * NW) headw_s[i] = a.head_w[i];
-    if (tid < a.ncls) headb_s[tid] = a.head_b[tid];
-  }
-  __syncthreads();
+  // per-block epilogue parameters into LDS with plain loads, issued after the first DMAs so
+  // the two latencies overlap (their vmcnt(0) also covers the DMAs; the prologue's barrier
+  // publishes them)
+  auto load_params = [&]() {
+    for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];
+    if (EPI == EPI_HEAD) {
+      for (int i = tid; i < a.ncls * 64; i += 64 * NW) headw_s[i] = a.head_w[i];
+      if (tid < a.ncls) headb_s[tid] = a.head_b[tid];
+    }
+  };
 
   // Halo rows owned by this lane are recomputed at every (once-per-chunk) halo issue
   // instead of being kept in ~3*HI registers; weight rows: one base pointer per lane.
@@ -564,6 +596,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   if constexpr (HSRC == 1) {
     issue_w(0);
     if (NS == 3 && total > 1) issue_w(1);
+    load_params();
     // --- fused down1.0: raw input window 20x20xC -> first conv on MFMA -> LDS halo ---
     float* xs = reinterpret_cast<float*>(lds + XS_OFF);
     int n0, ty0, tx0;
@@ -629,8 +662,9 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   issue_halo(0);
   issue_w(0);
   if (HB == 3 && hseq_end > 1) issue_halo(1);   // 3-deep ring: two chunks ahead from the start
+  if (NS == 3 && total > 1) issue_w(1);
+  load_params();
   if (NS == 3 && total > 1) {
-    issue_w(1);
     if (HB == 3 && hseq_end > 1) {
       if (wave < HLW) wait_vm_barrier<HI + WI>(); else wait_vm_barrier<WI>();
     } else {
@@ -701,14 +735,17 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
       read_frags(g, hseq, tap, 1, a1, b1);
       mfmas(a1, b1);
     }
-    // the next step needs W(g+1) (and, at a chunk end, the next halo, which is older);
-    // the barrier's lgkmcnt(0) also retires every fragment read of this step (WAR)
+    // the next step needs W(g+1) and, at a chunk end, the next halo.  That halo was issued
+    // (HB-1)*NTAP steps earlier; it is older than this step's loads except when it was issued
+    // in THIS step (HB = 2 ring over a single-tap GEMM, KT = 1), where the wait must cover it.
+    // The barrier's lgkmcnt(0) also retires every fragment read of this step (WAR).
+    constexpr bool kHaloNextStep = (HB - 1) * NTAP == 1;
     const unsigned long long st_b = stamp();
     if (PIPE == 4) {
       // ablation: no barrier
     } else if (NS == 2) {
       wait_vm_barrier<0>();
-    } else if (hnext && wave < HLW) {
+    } else if (hnext && wave < HLW && !kHaloNextStep) {
       if (wnext) wait_vm_barrier<HI + WI>(); else wait_vm_barrier<HI>();
     } else {
       if (wnext) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
@@ -975,6 +1012,12 @@ static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipSt
       case CFG_HALO1_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_HALO_R128_W8: return launch_halo<T, 2, 4, 4, 2, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_HALO1_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
+      case CFG_HALO1_R128T8_NS3: return launch_halo<T, 1, 4, 8, 1, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
+      // persistent 3-deep ring: a 1-tap GEMM step is short, so the next chunk is fetched two
+      // steps ahead (the 2-deep ring must wait for its prefetch at the end of the same step)
+      case CFG_HALO_R128_W4: return launch_halo<T, 1, 4, 8, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
+      case CFG_HALO3_R64_W8: return launch_halo<T, 1, 8, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
+      case CFG_HALO3_R64_W4: return launch_halo<T, 1, 4, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       default: return launch_cfg<T, 1, EPI_UPSCATTER>(cfg, a, s);
     }
   }

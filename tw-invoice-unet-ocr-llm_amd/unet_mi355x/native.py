@@ -49,6 +49,7 @@ SIGNATURES = {
     "unet_destroy": (_i, [_vp]),
     "unet_last_error": (ctypes.c_char_p, []),
     "unet_abi_version": (_i, []),
+    "unet_logit_cut": (ctypes.c_float, [ctypes.c_float]),
 }
 
 _lib = None
