@@ -130,8 +130,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layer-profile", action="store_true")
-    ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary (profiles/*.json) to fill roofline.traffic")
+    ap.add_argument("--traffic-json", default="auto",
+                    help="PMC summary (tools/pmc_summary.py output) to fill roofline.traffic; 'auto' = "
+                         "profiles/pmc_<dtype>_bs<batch>.json when present (collected by tools/gpu_round.sh)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -220,8 +221,11 @@ def main():
             k["algo_gb"] = round(k["algo_gb"], 2)
         peak = PEAK_TFLOPS[args.dtype]
         traffic = None
-        if args.traffic_json and os.path.exists(args.traffic_json):
-            tj = json.load(open(args.traffic_json))
+        tj_path = args.traffic_json
+        if tj_path == "auto":
+            tj_path = os.path.join(REPO, "profiles", f"pmc_{args.dtype}_bs{B}.json")
+        if tj_path and os.path.exists(tj_path) and S == 512:
+            tj = json.load(open(tj_path))
             traffic = tj.get(dom_name, {}).get("hbm_bytes_per_launch")
         roofline = {"bound": "mfma", "kernel": dom_name, "symbol": mangled(dom_name),
                     "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",

@@ -55,21 +55,31 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--out", default=None)
     ap.add_argument("--esize", type=int, default=2)
+    ap.add_argument("--bench-json", default=None,
+                    help="bench.py JSON line of the same build: launches it reports as fused_into_* issue no dispatch")
     a = ap.parse_args()
-    per_launch = [dict() for _ in LAUNCHES]
+    launches = list(LAUNCHES)
+    if a.bench_json:
+        kern = json.loads(open(a.bench_json).read().strip().splitlines()[-1])["kernels"]
+        fused = {l for k, v in kern.items() if k.startswith("fused_into") for l in v["layers"]}
+        launches = [e for e in LAUNCHES if e[0] not in fused]
+    per_launch = [dict() for _ in launches]
     for p in sorted(glob.glob(os.path.join(a.dir, "pass*"))):
         if not os.path.isdir(p):
             continue
         rows = load_pass(p)
         ours = [(did, v) for did, v in sorted(rows.items())
                 if "igemm" in v[0] or "first_conv" in v[0] or "halo" in v[0]]
-        last = ours[-len(LAUNCHES):]
+        last = ours[-len(launches):]
         for i, (did, (name, ctr)) in enumerate(last):
             per_launch[i].update(ctr)
             per_launch[i]["kernel_name"] = name
     print(f"{'launch':14s} {'read_GB':>8s} {'write_GB':>8s} {'algo_GB?':>8s} {'mfma_busy%':>10s} {'lds_conf%':>9s} {'wait_any%':>9s}")
     agg = defaultdict(lambda: defaultdict(float))
-    for e, c in zip(LAUNCHES, per_launch):
+    labels = {}
+    if a.bench_json:
+        labels = {l: k for k, v in kern.items() for l in v["layers"]}
+    for e, c in zip(launches, per_launch):
         rd = 2 * c.get("FETCH_SIZE", 0) * 1024
         wr = c.get("WRITE_SIZE", 0) * 1024
         busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0)
@@ -79,7 +89,7 @@ def main():
         wait = 100 * c.get("SQ_WAIT_ANY", 0) / max(1, c.get("SQ_WAVE_CYCLES", 0))
         algo = launch_bytes(e, a.batch, a.size, a.size, 3, a.esize)
         print(f"{e[0]:14s} {rd / 1e9:8.2f} {wr / 1e9:8.2f} {algo / 1e9:8.2f} {mfma_pct:10.1f} {conf:9.2f} {wait:9.1f}")
-        k = agg[label_of(c.get("kernel_name", e[1]))]
+        k = agg[labels.get(e[0]) or label_of(c.get("kernel_name", e[1]))]
         k["launches"] += 1
         k["hbm_read_bytes"] += rd
         k["hbm_write_bytes"] += wr
