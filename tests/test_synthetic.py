@@ -30,3 +30,30 @@ def test_invoice_pages_range_and_gray_replication():
     assert p.min() >= 0 and p.max() <= 1
     assert np.array_equal(p[:, 0], p[:, 1]) and np.array_equal(p[:, 0], p[:, 2])
     assert (p < 0.35).mean() > 0.002   # dark "text" rectangles exist
+
+
+def test_invoice_fields_follow_page_rectangles():
+    p = syn.invoice_pages(4, 2, 128, 128, 1)
+    f = syn.invoice_fields(4, 2, 128, 128)
+    assert f.shape == (2, 3, 128, 128) and f.dtype == np.uint8
+    on = f.max(axis=1).astype(bool)
+    # every field pixel lies on a dark rectangle (noise is N(0, 0.02) around values <= 0.3)
+    assert on.any() and (p[:, 0][on] < 0.45).all()
+    assert f[:, 2].sum() > 0 and f[:, 0].sum() > 0
+
+
+def test_pretrained_profile_is_the_structured_base_plus_the_committed_delta():
+    base = syn.make_state_dict(0, 3, 3, "structured")
+    pre = syn.make_state_dict(0, 3, 3, "pretrained")
+    assert list(pre) == list(base)
+    changed = [k for k in base if not np.array_equal(base[k], pre[k])]
+    assert changed and all((".net.1." in k or ".net.4." in k or k.startswith("up") or k.startswith("out_conv"))
+                           for k in changed)
+    assert all(not k.endswith("running_mean") and not k.endswith("running_var") for k in changed)
+    assert sum(pre[k].size for k in changed) < 20000
+    # 3x3 conv and ConvTranspose weights stay the seeded ones
+    assert np.array_equal(pre["conv4.net.0.weight"], base["conv4.net.0.weight"])
+    assert np.array_equal(pre["up1.weight"], base["up1.weight"])
+    one = syn.make_state_dict(0, 1, 3, "pretrained")
+    assert one["down1.net.0.weight"].shape == (64, 1, 3, 3)
+    assert np.array_equal(one["conv1.net.4.weight"], pre["conv1.net.4.weight"])

@@ -220,14 +220,23 @@ void put_elem(DType dt, std::vector<uint8_t>& buf, size_t idx, double v) {
 }
 
 // 3x3 layer: packed[rho][tap*cin + c] = W'[nat(rho)][c][ky][kx], tap = ky*3+kx
+// Ring kernels (cfg_is_ring) take the same rows in step order instead: per row tile of BR rows,
+// step s = (c / BKE) * 9 + tap holds a contiguous [BR][BKE] block (BKE = 64 bytes of K), so
+// packed[((ct * S + s) * BR + rho % BR) * BKE + c % BKE], S = 9 * cin / BKE.
 int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::vector<double>& b) {
   const int K = 9 * L.cin;
   std::vector<uint8_t> buf((size_t)L.cout * K * dtype_size(h->dt));
+  const bool ring = cfg_is_ring(L.cfg);
+  const int BR = cfg_rows(L.cfg), BKE = 64 / (int)dtype_size(h->dt), S = K / BKE;
+  if (ring && (L.cout % BR || L.cin % BKE)) return fail(UNET_EINVAL, "ring kernel tiling does not divide the layer");
   for (int rho = 0; rho < L.cout; ++rho) {
     const int o = natural_of_packed(rho);
     for (int tap = 0; tap < 9; ++tap)
-      for (int c = 0; c < L.cin; ++c)
-        put_elem(h->dt, buf, (size_t)rho * K + (size_t)tap * L.cin + c, w[((size_t)o * L.cin + c) * 9 + tap]);
+      for (int c = 0; c < L.cin; ++c) {
+        const size_t idx = ring ? (((size_t)(rho / BR) * S + (size_t)(c / BKE) * 9 + tap) * BR + rho % BR) * BKE + c % BKE
+                                : (size_t)rho * K + (size_t)tap * L.cin + c;
+        put_elem(h->dt, buf, idx, w[((size_t)o * L.cin + c) * 9 + tap]);
+      }
   }
   std::vector<float> bf(b.begin(), b.end());
   int rc = upload(h, &L.w, buf.data(), buf.size());
@@ -282,9 +291,13 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
       {2, 2, 4, 2, 3, 0}, {2, 4, 4, 2, 3, 0}, {1, 4, 4, 2, 3, 0}, {1, 8, 4, 2, 3, 0}, {1, 4, 4, 1, 3, 0},
       {1, 8, 4, 1, 3, 0}, {2, 2, 4, 1, 2, 0}, {2, 4, 4, 2, 3, 1}, {1, 4, 4, 1, 3, 1}, {1, 8, 4, 1, 3, 1},
       {1, 4, 8, 1, 2, 0}, {1, 4, 8, 1, 3, 0}, {1, 4, 4, 1, 3, 0}, {1, 8, 4, 1, 3, 0},
-      {1, 4, 4, 1, 3, 0}, {1, 4, 4, 2, 3, 0}, {1, 2, 4, 2, 3, 0}, {1, 8, 4, 3, 3, 0}, {1, 4, 4, 3, 3, 0}};
+      {1, 4, 4, 1, 3, 0}, {1, 4, 4, 2, 3, 0}, {1, 2, 4, 2, 3, 0}, {1, 8, 4, 3, 3, 0}, {1, 4, 4, 3, 3, 0},
+      {1, 4, 8, 1, 2, 7}, {1, 4, 8, 1, 3, 7}, {1, 4, 4, 1, 3, 7}, {1, 8, 4, 1, 3, 7}};
   if (cfg >= CFG_COUNT) {
     std::snprintf(buf, sizeof buf, "ablation_%d<%s, %d>", cfg - CFG_COUNT, tname(t), epi);
+  } else if (cfg_is_ring(cfg)) {
+    const int tc = cfg_rows(cfg) / 16, ns = (cfg == CFG_RING_R128_NS3) ? 3 : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
+    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d>", tname(t), tc, ns, epi);
   } else if (cfg_is_halo(cfg)) {
     const auto& c = halo[cfg - CFG_HALO_R128_W4];
     const int hsrc = (cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8) ? 1 : 0;
@@ -379,7 +392,9 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     if (ps == "gather") {
       L.cfg = L.cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
     } else {
-      L.cfg = kDefaultCfg[i];
+      // 16-bit: the 64-byte-row ring kernel on the 128-row layers (A/B: profiles/tune_r1_ring.txt);
+      // fp32 stays on the 128-byte halo kernel
+      L.cfg = (cfg->dtype != UNET_DTYPE_F32 && i >= 1 && i <= 14) ? (int)CFG_RING_R128_NS3 : kDefaultCfg[i];
     }
   }
   if (ps == "gather") h->L[C1B].cfg = CFG_R64_P128;
@@ -403,12 +418,15 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     const bool fused_in = L.cfg == CFG_FUSED_IN_W4 || L.cfg == CFG_FUSED_IN_W8;
     // fall back within the same kernel family (LDS-halo configurations all accumulate in the
     // same K order, so they agree bitwise; the gather kernels order K differently)
-    const bool halo = cfg_is_halo(L.cfg);
+    // (the ring kernels share one K order among themselves, chunk32-major)
+    const bool ring = cfg_is_ring(L.cfg);
+    const bool halo = cfg_is_halo(L.cfg) && !ring;
     if (fused_in && (i != D1B || cfg->dtype == UNET_DTYPE_F32))
       L.cfg = L.cout == 64 ? CFG_HALO1_R64_W8 : CFG_HALO1_R128T8_NS2;
     if (cfg_rows(L.cfg) > L.cout || L.cfg == CFG_R128_P256 || (cfg_single_chunk(L.cfg) && L.cin != chunk))
-      L.cfg = L.cout == 64 ? (halo ? CFG_HALO1_R64_W8 : CFG_R64_P256) : (halo ? CFG_HALO1_R128T8_NS2 : CFG_R128_P128);
-    if (i == C1B && cfg_rows(L.cfg) != 64) L.cfg = halo ? CFG_HALO1_R64_W8 : CFG_R64_P128;
+      L.cfg = L.cout == 64 ? (ring ? CFG_RING_R64 : halo ? CFG_HALO1_R64_W8 : CFG_R64_P256)
+                           : (ring ? CFG_RING_R128_NS3 : halo ? CFG_HALO1_R128T8_NS2 : CFG_R128_P128);
+    if (i == C1B && cfg_rows(L.cfg) != 64) L.cfg = ring ? CFG_RING_R64 : halo ? CFG_HALO1_R64_W8 : CFG_R64_P128;
   }
   build_labels(h);
   for (int i = 0; i < 4; ++i) {
@@ -431,7 +449,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
         if (li >= 0 && li < 4 && (c == CFG_R128_P128 || c == CFG_R64_P128 || c == CFG_HALO1_R64_W4 ||
                                   c == CFG_HALO1_R128T8_NS2 || c == CFG_HALO_R128_W8 || c == CFG_HALO1_R64_W8 ||
                                   c == CFG_HALO1_R128T8_NS3 || c == CFG_HALO_R128_W4 || c == CFG_HALO3_R64_W8 ||
-                                  c == CFG_HALO3_R64_W4))
+                                  c == CFG_HALO3_R64_W4 || c == CFG_SG_R128T8_NS2 || c == CFG_SG_R64_W4))
           h->U[li].cfg = c;
       }
       pos = end + 1;

@@ -31,11 +31,13 @@ typedef int frag_t __attribute__((ext_vector_type(4)));   // one 16-byte MFMA op
 
 int cfg_rows(int cfg) {
 #ifdef UNET_ABLATION
-  if (cfg >= CFG_COUNT) return (cfg == CFG_COUNT + 2 || cfg == CFG_COUNT + 3 || cfg == CFG_COUNT + 9) ? 128 : 64;
+  if (cfg >= CFG_COUNT)
+    return (cfg == CFG_COUNT + 2 || cfg == CFG_COUNT + 3 || cfg == CFG_COUNT + 9 || cfg >= CFG_COUNT + 11) ? 128 : 64;
 #endif
   return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8 ||
           cfg == CFG_HALO1_R128_W4 || cfg == CFG_PHALO_R128_W8 || cfg == CFG_HALO1_R128T8_NS2 ||
-          cfg == CFG_HALO1_R128T8_NS3) ? 128 : 64;
+          cfg == CFG_HALO1_R128T8_NS3 || cfg == CFG_SG_R128T8_NS2 || cfg == CFG_SG_R128T8_NS3 ||
+          cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3) ? 128 : 64;
 }
 bool cfg_single_chunk(int cfg) { (void)cfg; return false; }
 int cfg_pixels(int cfg) {
@@ -43,9 +45,10 @@ int cfg_pixels(int cfg) {
           cfg == CFG_T8_HALO_R64_W2) ? 128 : 256;
 }
 bool cfg_is_halo(int cfg) { return cfg >= CFG_HALO_R128_W4; }
+bool cfg_is_ring(int cfg) { return cfg >= CFG_RING_R128 && cfg <= CFG_RING_R64_NS5; }
 int cfg_limit() {
 #ifdef UNET_ABLATION
-  return CFG_COUNT + 11;
+  return CFG_COUNT + 15;
 #else
   return CFG_COUNT;
 #endif
@@ -707,6 +710,48 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
 #pragma unroll
     for (int p = 0; p < TP; ++p) asm volatile("" : "+v"(bf[p]) : : "memory");
   };
+  // PIPE 7: one step as a fixed read/MFMA interleave.  The A (weight) fragments stream
+  // through a 3-register ring, each read two MFMA groups ahead of its use; the B (halo)
+  // fragments of kk = 1 are read during the kk = 0 groups.  sched_group_barrier pins the
+  // order, so the waits in front of each MFMA group cover only reads issued >= 2 groups
+  // earlier (hipcc's default schedule under register pressure reuses ONE A register and
+  // waits lgkmcnt(0) in front of every group).
+  auto step_sg = [&](int g, int hs, int tp) {
+    const int dy = tp / KT, dx = tp - (tp / KT) * KT;
+    const char* Hs = lds + (hs % HB) * HALO_BYTES;
+    const char* Ws = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 128;
+    const int toff = dy * HWD + dx;
+    const int hx7 = (px_lane + dx) & 7;
+    const int l7 = lane & 7;
+    constexpr int NI = 2 * TC;
+    frag_t bq[2][TP], ar[3];
+    auto rdA = [&](int i) {
+      const int kk = i / TC, t = i - (i / TC) * TC;
+      return *reinterpret_cast<const frag_t*>(Ws + t * 16 * 128 + (((kk * 4 + q) ^ l7) << 4));
+    };
+    auto rdB = [&](int kk, int p) {
+      return *reinterpret_cast<const frag_t*>(Hs + (prow[p] + toff) * 128 + (((kk * 4 + q) ^ hx7) << 4));
+    };
+#pragma unroll
+    for (int p = 0; p < TP; ++p) bq[0][p] = rdB(0, p);
+    ar[0] = rdA(0);
+    ar[1] = rdA(1);
+    __builtin_amdgcn_sched_group_barrier(0x100, TP + 2, 0);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      int nr = 0;
+      if (i + 2 < NI) { ar[(i + 2) % 3] = rdA(i + 2); ++nr; }
+      if (i >= 1 && i <= TP) { bq[1][i - 1] = rdB(1, i - 1); ++nr; }
+      const frag_t a = ar[i % 3];
+#pragma unroll
+      for (int p = 0; p < TP; ++p)
+        mfma_frag<T>(acc[i % TC][p], __builtin_bit_cast(uint4, a), __builtin_bit_cast(uint4, bq[i / TC][p]));
+      if (nr == 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // i is unrolled: nr folds
+      else if (nr == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+    }
+  };
+
   frag_t a0[TC], b0[TP], a1[TC], b1[TP];
   if (PIPE == 1 || PIPE == 5) read_frags(0, 0, 0, 0, a0, b0);
 
@@ -717,12 +762,16 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     // ring of HB halo buffers: at a chunk's first tap, prefetch the halo HB-1 chunks ahead
     const bool hnext = HB >= 2 && (tap == 0) && (hseq + HB - 1 < hseq_end);
     const bool wnext = g + NS - 1 < total;
-    constexpr bool kDma = PIPE < 3;       // ablations 3, 4, 5: no DMA in the loop
+    constexpr bool kDma = PIPE < 3 || PIPE > 5;   // ablations 3, 4, 5: no DMA in the loop
+    constexpr bool kDmaW = kDma && PIPE != 8;     // ablation 8: halo DMA only
+    constexpr bool kDmaH = kDma && PIPE != 9;     // ablation 9: weight DMA only
     constexpr bool kPipe = PIPE == 1 || PIPE == 5;
-    if (kDma && hnext) issue_halo(hseq + HB - 1);
-    if (kDma && wnext) issue_w(g + NS - 1);
+    if (kDmaH && hnext) issue_halo(hseq + HB - 1);
+    if (kDmaW && wnext) issue_w(g + NS - 1);
 
-    if (kPipe) {
+    if constexpr (PIPE == 7) {
+      step_sg(g, hseq, tap);
+    } else if (kPipe) {
       // kk=1 reads in flight behind the kk=0 MFMAs; kk=0 of the next step is read right
       // after the barrier, behind this step's kk=1 MFMAs: no read-latency bubble per step.
       read_frags(g, hseq, tap, 1, a1, b1);
@@ -751,7 +800,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
       if (wnext) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
     }
     if (HB == 1 && tap == NTAP - 1 && hseq + 1 < hseq_end) {
-      if (kDma) issue_halo(hseq + 1);   // every wave has finished reading the halo (barrier above)
+      if (kDmaH) issue_halo(hseq + 1);   // every wave has finished reading the halo (barrier above)
       wait_vm_barrier<0>();
     }
 
@@ -799,6 +848,250 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     if (lane == 0 && a.dbg) {
       unsigned long long* d = a.dbg + ((size_t)blockIdx.x * NW + wave) * 8;
       d[0] = st_pro; d[1] = st_cmp; d[2] = st_wait; d[3] = st_epi; d[4] = tot; d[5] = st_steps; d[6] = 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// 3x3 conv, ring pipeline over 32-channel (64-byte) K chunks (the main kernel for 3x3 layers)
+// ---------------------------------------------------------------------------------
+// The 128-byte-row halo kernel above keeps one 64-channel halo (41.5 KB) and two weight slots
+// in LDS, so two blocks fit per CU but the next chunk's halo load is exposed and the weights
+// are fetched only one step ahead -- ablations (profiles/tune_r1_ring.txt) put ~25 % of the
+// time of the MFMA-bound layers in those waits.  Halving the row to 64 bytes (32 bf16/f16
+// channels, 16 f32) halves every LDS image, which buys, at the same two blocks per CU:
+//   * a double-buffered halo: the next chunk's 18x18 halo streams in during the current
+//     chunk's nine taps (issued at tap 0, needed 9 steps later);
+//   * an NS-slot weight ring: each step's weights are fetched NS-1 steps ahead.
+// LDS: [halo 0][halo 1][w slot 0..NS-1][bias/head params] = 2*21 KB + NS*BR*64 B (+2 KB).
+// A step = (chunk c32, tap): one MFMA K-block (16x16x32 bf16/f16; 4 x 16x16x4 f32) for each of
+// the TC x TP fragment pairs of the wave.  The weights are pre-packed per row tile in step
+// order ([ct][step][BR][64 B], unet_capi.cpp pack3x3) so every weight DMA instruction reads
+// 1 KB contiguous.  Bank-conflict-free 64-byte-row images: halo pixel (hy,hx) chunk q at
+// position q ^ (hx & 3); weight row r chunk q at position q ^ ((r >> 1) & 3) (exhaustive check
+// over all ds_read_b128 lane groups, taps and pixel groups: tools/swizzle_check.py).
+// Blocks are persistent (n_ct row tiles x n_slots walkers, each walking pixel tiles slot,
+// slot + n_slots, ...) so the rings run across tile boundaries and the epilogue of one tile
+// overlaps the loads of the next.
+constexpr int kRingPix = 18 * 18;
+
+template <typename T, int WR, int WPX, int TCW, int NS>
+struct RingGeom {
+  static constexpr int NW = WR * WPX;
+  static constexpr int TC = TCW;
+  static constexpr int TP = 16 / WPX;               // 16-pixel groups per wave (16 per tile)
+  static constexpr int BR = WR * 16 * TC;
+  static constexpr int BKE = 64 / (int)sizeof(T);   // K elements per step (64 bytes)
+  static constexpr int RPI = 16;                    // 64-byte rows per LDS-DMA instruction
+  static constexpr int HLW = NW >= 7 ? 7 : (NW >= 3 ? 3 : NW);   // halo loader waves (21 instr.)
+  static constexpr int HI = (kRingPix + RPI * HLW - 1) / (RPI * HLW);
+  static constexpr int HALO_BYTES = HI * HLW * RPI * 64;
+  static constexpr int WI = BR / (RPI * NW);
+  static constexpr int WSLOT = BR * 64;
+  static constexpr int WOFF = 2 * HALO_BYTES;
+  static constexpr int PARAM_OFF = WOFF + NS * WSLOT;
+  static constexpr int LDS_BYTES = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
+  static constexpr int BLOCKS_PER_CU = (160 * 1024) / LDS_BYTES;
+};
+
+// vmcnt(N) + barrier with N = nw * WI + (halo ? HI : 0), nw in [0, NS-2], as compile-time counts
+template <int N>
+__device__ __forceinline__ void wait_vm_only() {   // ablation: the wait without the barrier
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+  asm volatile("" ::: "memory");
+}
+template <int WI, int HI, int NSM2>
+__device__ __forceinline__ void ring_wait_nobar(int nw, bool halo) {
+  if constexpr (NSM2 >= 2) { if (nw == 2) { if (halo) wait_vm_only<2 * WI + HI>(); else wait_vm_only<2 * WI>(); return; } }
+  if constexpr (NSM2 >= 1) { if (nw == 1) { if (halo) wait_vm_only<WI + HI>(); else wait_vm_only<WI>(); return; } }
+  if (halo) wait_vm_only<HI>(); else wait_vm_only<0>();
+}
+template <int WI, int HI, int NSM2>
+__device__ __forceinline__ void ring_wait(int nw, bool halo) {
+  if constexpr (NSM2 >= 3) { if (nw == 3) { if (halo) wait_vm_barrier<3 * WI + HI>(); else wait_vm_barrier<3 * WI>(); return; } }
+  if constexpr (NSM2 >= 2) { if (nw == 2) { if (halo) wait_vm_barrier<2 * WI + HI>(); else wait_vm_barrier<2 * WI>(); return; } }
+  if constexpr (NSM2 >= 1) { if (nw == 1) { if (halo) wait_vm_barrier<WI + HI>(); else wait_vm_barrier<WI>(); return; } }
+  if (halo) wait_vm_barrier<HI>(); else wait_vm_barrier<0>();
+}
+
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0>
+__global__ __launch_bounds__(64 * WR * WPX, 2) void conv3x3_ring_kernel(const IgemmArgs a) {
+  using G = RingGeom<T, WR, WPX, TCW, NS>;
+  constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
+  constexpr int HI = G::HI, WI = G::WI, HLW = G::HLW, HALO_BYTES = G::HALO_BYTES, WSLOT = G::WSLOT;
+  constexpr int WOFF = G::WOFF;
+  static_assert(NS >= 3 && NS <= 5, "weight ring depth");
+  static_assert(WI >= 1 && BR % (G::RPI * NW) == 0, "weight tile split");
+  static_assert(TP >= 1 && 16 % WPX == 0, "pixel groups per wave");
+  static_assert(EPI != EPI_HEAD || BR == 64, "fused head needs the 64 channels in one block");
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
+  float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
+  float* headw_s = bias_s + BR;
+  float* headb_s = headw_s + kMaxClasses * 64;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wr = wave / WPX;
+  const int wp = wave % WPX;
+
+  int bid;
+  {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one pixel-tile walker
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
+    const int b = blockIdx.x, x = b & 7, k = b >> 3;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  }
+  const int ct = bid % a.n_ct;
+  const int slot = bid / a.n_ct;
+  const int n_slots = gridDim.x / a.n_ct;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  if (slot >= n_mt) return;
+  const int items = (n_mt - slot + n_slots - 1) / n_slots;
+
+  const int H = a.H, W = a.W;
+  const int nch = a.Cin / BKE;
+  const int S = 9 * nch;
+  const int total = items * S;
+  const int hseq_end = items * nch;
+
+  // weights of row tile ct in step order: step s at wblk + s * WSLOT; per lane one 16-byte
+  // chunk of row (wave*WI + j)*16 + lane/4, stored at position lane&3 = chunk ^ ((row>>1)&3)
+  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * WSLOT +
+                     (wave * WI * 16 + (lane >> 2)) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
+  const char* in = reinterpret_cast<const char*>(a.in);
+  const char* zero = reinterpret_cast<const char*>(a.zero);
+
+  auto tile_of = [&](int i, int& n, int& ty, int& tx) {
+    int mt = slot + i * n_slots;
+    tx = mt % a.tiles_x;
+    mt /= a.tiles_x;
+    ty = mt % a.tiles_y;
+    n = mt / a.tiles_y;
+  };
+  auto issue_halo = [&](int hseq) {
+    if (wave >= HLW) return;   // (wave-uniform) not a halo loader
+    const int i = hseq / nch, c = hseq - (hseq / nch) * nch;
+    int n, ty, tx;
+    tile_of(i, n, ty, tx);
+    char* dst = lds + (hseq & 1) * HALO_BYTES + wave * HI * 1024;
+    const long long c0 = (long long)c * BKE;
+    const long long pix0 = (long long)(n * H + ty * 16) * W + tx * 16;
+#pragma unroll
+    for (int j = 0; j < HI; ++j) {
+      const int row = (wave * HI + j) * 16 + (lane >> 2);
+      const int hy = row / 18, hx = row - (row / 18) * 18;
+      const int iy = ty * 16 + hy - 1, ix = tx * 16 + hx - 1;
+      const bool ok = row < kRingPix && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const int chk = ((lane & 3) ^ (hx & 3)) << 4;
+      const long long pix = pix0 + (long long)(hy - 1) * W + (hx - 1);
+      const char* src = ok ? in + (pix * a.ldi + c0) * (long long)sizeof(T) + chk : zero + chk;
+      glds16(src, dst + j * 1024);
+    }
+  };
+  auto issue_w = [&](int g) {
+    const int s = g - (g / S) * S;
+    const char* src = wblk + (size_t)s * WSLOT;
+    char* dst = lds + WOFF + (g % NS) * WSLOT + wave * WI * 1024;
+#pragma unroll
+    for (int j = 0; j < WI; ++j) glds16(src + j * 1024, dst + j * 1024);
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int t = 0; t < TC; ++t)
+#pragma unroll
+    for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int col = lane & 15, q = lane >> 4;
+  int prow[TP];
+#pragma unroll
+  for (int p = 0; p < TP; ++p) {
+    int py, px;
+    pix_of((wp * TP + p) * 16 + col, py, px);
+    prow[p] = (py * 18 + px) * 64;
+  }
+  const int px_lane = col & 7;
+  const int wpos = (q ^ ((col >> 1) & 3)) << 4;
+  const char* wrow = lds + WOFF + (wr * 16 * TC + col) * 64 + wpos;
+
+  // prologue: halo of chunk 0 and weights of steps 0 .. NS-2
+  issue_halo(0);
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (k < total) issue_w(k);
+  for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];
+  if (EPI == EPI_HEAD) {
+    for (int i = tid; i < a.ncls * 64; i += 64 * NW) headw_s[i] = a.head_w[i];
+    if (tid < a.ncls) headb_s[tid] = a.head_b[tid];
+  }
+  {
+    const int young = total - 1 < NS - 2 ? total - 1 : NS - 2;   // W(1..NS-2) may stay in flight
+    ring_wait<WI, HI, NS - 2>(young, false);
+  }
+
+  // one step: A (weight) fragments stream through a 3-register ring two MFMA groups ahead;
+  // sched_group_barrier pins the read/MFMA interleave (see step_sg above)
+  auto step = [&](int g, int hs, int tp) {
+    const int dy = tp / 3, dx = tp - (tp / 3) * 3;
+    const char* Hs = lds + (hs & 1) * HALO_BYTES + (dy * 18 + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
+    const char* Ws = wrow + (g % NS) * WSLOT;
+    frag_t bq[TP], ar[3];
+#pragma unroll
+    for (int p = 0; p < TP; ++p) bq[p] = *reinterpret_cast<const frag_t*>(Hs + prow[p]);
+    ar[0] = *reinterpret_cast<const frag_t*>(Ws);
+    if (TC > 1) ar[1] = *reinterpret_cast<const frag_t*>(Ws + 16 * 64);
+    __builtin_amdgcn_sched_group_barrier(0x100, TP + (TC > 1 ? 2 : 1), 0);
+#pragma unroll
+    for (int t = 0; t < TC; ++t) {
+      if (t + 2 < TC) ar[(t + 2) % 3] = *reinterpret_cast<const frag_t*>(Ws + (t + 2) * 16 * 64);
+      const frag_t af = ar[t % 3];
+#pragma unroll
+      for (int p = 0; p < TP; ++p)
+        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
+      if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+    }
+  };
+
+  int c = 0, tap = 0, hseq = 0, item = 0;
+  for (int g = 0; g < total; ++g) {
+    const bool hnext = tap == 0 && hseq + 1 < hseq_end;
+    if (hnext) issue_halo(hseq + 1);
+    if (g + NS - 1 < total) issue_w(g + NS - 1);
+    step(g, hseq, tap);
+    // W(g+1) must have landed (and, at a chunk end, the next halo -- issued 8 steps earlier,
+    // so older than W(g+1)).  Younger loads may stay in flight: W(g+2 .. g+NS-1) and a halo
+    // issued within the last NS-2 steps (this chunk's tap < NS-2).
+    {
+      int young = total - 2 - g;
+      young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
+      const bool hyoung = wave < HLW && tap < NS - 2 && hseq + 1 < hseq_end;
+      if (ABL == 1 && tap != 8) ring_wait_nobar<WI, HI, NS - 2>(young, hyoung);   // ablation: barrier per chunk only
+      else ring_wait<WI, HI, NS - 2>(young, hyoung);
+    }
+    bool tile_end = false;
+    if (++tap == 9) {
+      tap = 0;
+      ++hseq;
+      if (++c == nch) {
+        c = 0;
+        tile_end = true;
+      }
+    }
+    if (tile_end) {
+      int n, ty, tx;
+      tile_of(item, n, ty, tx);
+#pragma unroll
+      for (int h = 0; h < TC / 4; ++h)
+        conv_epilogue<T, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
+                                  wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h,
+                                  headw_s, headb_s);
+#pragma unroll
+      for (int t = 0; t < TC; ++t)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ++item;
     }
   }
 }
@@ -942,6 +1235,22 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0>
+static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
+  using G = RingGeom<T, WR, WPX, TCW, NS>;
+  if constexpr (EPI == EPI_HEAD && G::BR != 64) return hipErrorInvalidValue;
+  if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
+  if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  int n_slots = (kNumCUs * G::BLOCKS_PER_CU) / a.n_ct;
+  if (n_slots < 1) n_slots = 1;
+  if (n_slots > n_mt) n_slots = n_mt;
+  if constexpr (EPI != EPI_HEAD || G::BR == 64)
+    hipLaunchKernelGGL((conv3x3_ring_kernel<T, WR, WPX, TCW, NS, EPI, ABL>), dim3(a.n_ct * n_slots), dim3(64 * WR * WPX), 0,
+                       s, a);
+  return hipGetLastError();
+}
+
 template <typename T, int TAPS, int EPI>
 static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
   if constexpr (TAPS == 9) {
@@ -963,6 +1272,14 @@ static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
       case CFG_T8_HALO_R64_W2: return launch_halo<T, 1, 2, 4, 2, 3, 0, EPI, 0, 3, 8>(a, s);
       case CFG_HALO3_R64_W8: return launch_halo<T, 1, 8, 4, 3, 3, 0, EPI>(a, s);
       case CFG_HALO3_R64_W4: return launch_halo<T, 1, 4, 4, 3, 3, 0, EPI>(a, s);
+      case CFG_SG_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 7, EPI>(a, s);
+      case CFG_SG_R128T8_NS3: return launch_halo<T, 1, 4, 8, 1, 3, 7, EPI>(a, s);
+      case CFG_SG_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 7, EPI>(a, s);
+      case CFG_SG_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 7, EPI>(a, s);
+      case CFG_RING_R128: return launch_ring<T, 1, 4, 8, 4, EPI>(a, s);
+      case CFG_RING_R64: return launch_ring<T, 1, 4, 4, 4, EPI>(a, s);
+      case CFG_RING_R128_NS3: return launch_ring<T, 1, 4, 8, 3, EPI>(a, s);
+      case CFG_RING_R64_NS5: return launch_ring<T, 1, 4, 4, 5, EPI>(a, s);
       case CFG_FUSED_IN_W4:
       case CFG_FUSED_IN_W8:
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) {
@@ -982,6 +1299,10 @@ static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
       case CFG_COUNT + 8: return launch_halo<T, 1, 8, 4, 1, 3, 6, EPI>(a, s);   // stamped HALO1_R64_W8
       case CFG_COUNT + 9: return launch_halo<T, 1, 4, 8, 1, 2, 6, EPI>(a, s);   // stamped HALO1_R128T8_NS2
       case CFG_COUNT + 10: return launch_halo<T, 1, 8, 4, 3, 3, 6, EPI>(a, s);  // stamped HALO3_R64_W8
+      case CFG_COUNT + 11: return launch_halo<T, 1, 4, 8, 1, 2, 8, EPI>(a, s);  // HALO1_R128T8_NS2, halo DMA only
+      case CFG_COUNT + 12: return launch_halo<T, 1, 4, 8, 1, 2, 9, EPI>(a, s);  // HALO1_R128T8_NS2, weight DMA only
+      case CFG_COUNT + 13: return launch_halo<T, 1, 4, 8, 1, 2, 3, EPI>(a, s);  // HALO1_R128T8_NS2, no DMA
+      case CFG_COUNT + 14: return launch_ring<T, 1, 4, 8, 4, EPI, 1>(a, s);      // RING_R128, barrier per chunk only
 #endif
       default: break;
     }
@@ -1013,6 +1334,8 @@ static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipSt
       case CFG_HALO_R128_W8: return launch_halo<T, 2, 4, 4, 2, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_HALO1_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_HALO1_R128T8_NS3: return launch_halo<T, 1, 4, 8, 1, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
+      case CFG_SG_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 7, EPI_UPSCATTER, 0, 1>(a, s);
+      case CFG_SG_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 7, EPI_UPSCATTER, 0, 1>(a, s);
       // persistent 3-deep ring: a 1-tap GEMM step is short, so the next chunk is fetched two
       // steps ahead (the 2-deep ring must wait for its prefetch at the end of the same step)
       case CFG_HALO_R128_W4: return launch_halo<T, 1, 4, 8, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);

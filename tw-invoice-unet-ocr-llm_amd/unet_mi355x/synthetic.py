@@ -14,6 +14,7 @@ State-dict layout (136 keys, registration order) follows
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -26,6 +27,7 @@ _M2 = np.uint64(0x94D049BB133111EB)
 DOUBLE_CONVS = ("down1", "down2", "down3", "down4", "bottleneck",
                 "conv4", "conv3", "conv2", "conv1")
 UPS = ("up4", "up3", "up2", "up1")
+PRETRAINED_DELTA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "pretrained_delta.npz")
 
 
 def _fnv1a64(s: str) -> int:
@@ -122,7 +124,27 @@ def make_state_dict(seed: int = 0, n_channels: int = 3, n_classes: int = 3,
       as unet_model.py:52-53) -- logits sit near -4, every mask is empty.
     profile "structured": He-normal conv weights, randomised eval BN statistics,
       so activations stay O(1) through all 19 layers and masks are non-trivial.
+    profile "pretrained": the seed-0 structured weights with the ~13 k BatchNorm-affine /
+      ConvTranspose-bias / out_conv parameters replaced by the values fine-tuned on the
+      synthetic invoice fields (tools/pretrain_synthetic.py, data/pretrained_delta.npz):
+      a trained-like, bimodal logit distribution for mask-IoU measurements.
     """
+    if profile == "pretrained":
+        if seed != 0 or n_classes != 3 or base != 64:
+            raise ValueError("profile 'pretrained' exists for seed 0, n_classes 3, base 64 only")
+        sd = make_state_dict(0, n_channels, 3, "structured", None, 64)
+        z = np.load(PRETRAINED_DELTA)
+        if n_channels == 3 and bytes(z["__base_checksum__"]).decode() != state_dict_checksum(sd):
+            raise RuntimeError("pretrained delta was made for different base weights")
+        for k in z.files:
+            if k.startswith("__"):
+                continue
+            if sd[k].shape != z[k].shape:
+                raise RuntimeError(f"pretrained delta: shape mismatch for {k}")
+            sd[k] = np.asarray(z[k], dtype=np.float32)
+        if out_bias is not None:
+            sd["out_conv.bias"] = np.full(n_classes, float(out_bias), dtype=np.float32)
+        return sd
     sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
     for key, shape in unet_shapes(n_channels, n_classes, base):
         n = int(np.prod(shape)) if shape else 1
@@ -181,6 +203,23 @@ def uniform_batch(seed: int, n: int, c: int, h: int, w: int) -> np.ndarray:
     return uniform(seed, "input.uniform", n * c * h * w).astype(np.float32).reshape(n, c, h, w)
 
 
+def _page_rects(seed: int, i: int, h: int, w: int, rects_per_512sq: int):
+    """Background level and the (y0, x0, rh, rw, value) rectangles of page i."""
+    key = f"page.{i}"
+    sy, sx = h / 512.0, w / 512.0
+    nrect = max(1, int(round(rects_per_512sq * h * w / (512.0 * 512.0))))
+    bg = 0.8 + 0.2 * uniform(seed, key + ".bg", 1)[0]
+    r = uniform(seed, key + ".rects", nrect * 5).reshape(nrect, 5)
+    rects = []
+    for k in range(nrect):
+        rh = max(1, int((6 + 34 * r[k, 0]) * sy))
+        rw = max(1, int((20 + 180 * r[k, 1]) * sx))
+        y0 = int(r[k, 2] * max(1, h - rh))
+        x0 = int(r[k, 3] * max(1, w - rw))
+        rects.append((y0, x0, rh, rw, 0.3 * r[k, 4]))
+    return bg, rects
+
+
 def invoice_pages(seed: int, n: int, h: int = 512, w: int = 512, channels: int = 3,
                   rects_per_512sq: int = 40) -> np.ndarray:
     """Invoice-like gray pages, fp32 NCHW in [0,1] (SURVEY.md §8d distribution 2).
@@ -191,21 +230,34 @@ def invoice_pages(seed: int, n: int, h: int = 512, w: int = 512, channels: int =
     for a grayscale photo (inference.py:35).
     """
     out = np.empty((n, 1, h, w), dtype=np.float32)
-    sy, sx = h / 512.0, w / 512.0
-    nrect = max(1, int(round(rects_per_512sq * h * w / (512.0 * 512.0))))
     for i in range(n):
-        key = f"page.{i}"
-        bg = 0.8 + 0.2 * uniform(seed, key + ".bg", 1)[0]
+        bg, rects = _page_rects(seed, i, h, w, rects_per_512sq)
         page = np.full((h, w), bg, dtype=np.float64)
-        r = uniform(seed, key + ".rects", nrect * 5).reshape(nrect, 5)
-        for k in range(nrect):
-            rh = max(1, int((6 + 34 * r[k, 0]) * sy))
-            rw = max(1, int((20 + 180 * r[k, 1]) * sx))
-            y0 = int(r[k, 2] * max(1, h - rh))
-            x0 = int(r[k, 3] * max(1, w - rw))
-            page[y0:y0 + rh, x0:x0 + rw] = 0.3 * r[k, 4]
-        page += 0.02 * normal(seed, key + ".noise", h * w).reshape(h, w)
+        for y0, x0, rh, rw, v in rects:
+            page[y0:y0 + rh, x0:x0 + rw] = v
+        page += 0.02 * normal(seed, f"page.{i}.noise", h * w).reshape(h, w)
         out[i, 0] = np.clip(page, 0.0, 1.0)
     if channels == 1:
         return out
     return np.ascontiguousarray(np.repeat(out, channels, axis=1))
+
+
+def invoice_fields(seed: int, n: int, h: int = 512, w: int = 512,
+                   rects_per_512sq: int = 40) -> np.ndarray:
+    """Synthetic field masks [n, 3, h, w] (uint8) for the pages of ``invoice_pages``.
+
+    A stand-in for the three trained fields (``inference.py:12``: invoice_no, date,
+    total_amount), defined by rectangle geometry so that a segmentation net can learn them:
+    field 0 = tall rectangles (height >= 20 px per 512), field 1 = wide ones (width >= 110),
+    field 2 = the darkest ones (value < 0.15).  Later rectangles overwrite earlier ones,
+    as on the page.  Used only to give the synthetic weights a trained-like (bimodal)
+    logit distribution (tools/pretrain_synthetic.py).
+    """
+    out = np.zeros((n, 3, h, w), dtype=np.uint8)
+    sy, sx = h / 512.0, w / 512.0
+    for i in range(n):
+        _, rects = _page_rects(seed, i, h, w, rects_per_512sq)
+        for y0, x0, rh, rw, v in rects:
+            out[i, :, y0:y0 + rh, x0:x0 + rw] = np.array(
+                [rh >= 20 * sy, rw >= 110 * sx, v < 0.15], dtype=np.uint8)[:, None, None]
+    return out
