@@ -96,6 +96,19 @@ int unet_forward(unet_handle* h, const void* x, int x_layout, int x_dtype,
                  void* logits, void* masks, int mask_kind,
                  int N, int H, int W, void* hip_stream);
 
+/* unet_forward, plus the bounding box of every (image, field) mask -- the np.where ->
+ * min/max step of run_unet (inference.py:84-90) on the device, so a caller that only needs
+ * the crop rectangles copies 16 bytes per field instead of the mask (and a multi-GPU caller
+ * all-gathers 48 bytes per image).
+ * boxes: device int32 [N][n_classes][4] = x_min, y_min, x_max, y_max in mask pixels
+ *        (inclusive), all four -1 for an empty mask.
+ * masks / mask_kind as for unet_forward; when masks is NULL (or mask_kind is
+ * UNET_MASK_NONE) the masks go to the workspace and only the boxes are returned.
+ * Replaces: UNet.forward + inference.py:72-90. */
+int unet_forward_boxes(unet_handle* h, const void* x, int x_layout, int x_dtype,
+                       void* logits, void* masks, int mask_kind, int32_t* boxes,
+                       int N, int H, int W, void* hip_stream);
+
 /* Number of kernel launches in one forward (first conv, 17 implicit-GEMM 3x3 convs with
  * the fused pool / head epilogues, 4 ConvTranspose2d), in execution order:
  * down1.0 down1.3 down2.0 down2.3 down3.0 down3.3 down4.0 down4.3 bottleneck.0

@@ -26,6 +26,14 @@ def fake_masks(x):
             ).expand(-1, 3, 4, 8).contiguous()
 
 
+def fake_boxes(x):
+    # unet_forward_boxes-shaped output: int32 [n, 3, 4], -1s for "empty" fields
+    v = (x.sum(dim=(1, 2, 3)).abs() * 10).floor().to(torch.int32)
+    b = torch.stack([v, v + 1, v + 2, v + 3], -1).unsqueeze(1).repeat(1, 3, 1)
+    b[v % 3 == 0, 1] = -1
+    return b.contiguous()
+
+
 def _worker(rank, world, port, n_total, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -38,7 +46,9 @@ def _worker(rank, world, port, n_total, q):
         ref = fake_masks(x)
         lo, hi = shard_bounds(n_total, rank, world)
         got2 = seg(x[lo:hi], n_total=n_total, already_local=True)
-        q.put((rank, bool(torch.equal(got, ref)), bool(torch.equal(got2, ref))))
+        boxes = ShardedSegmenter(fake_boxes)(x)     # the 48-byte-per-image gather of §8f
+        ok2 = bool(torch.equal(got2, ref)) and bool(torch.equal(boxes, fake_boxes(x)))
+        q.put((rank, bool(torch.equal(got, ref)), ok2))
     finally:
         dist.destroy_process_group()
 

@@ -280,3 +280,62 @@ def test_forward_deterministic_and_config_invariant(dtype, monkeypatch):
             bad.append((None, up, d[:3]))
     print(bad)
     assert bad == []
+
+
+def _np_boxes(masks):
+    """[N, C, H, W] bool -> int32 [N, C, 4] (x_min, y_min, x_max, y_max), -1s if empty."""
+    out = np.full(masks.shape[:2] + (4,), -1, dtype=np.int32)
+    for i in range(masks.shape[0]):
+        for c in range(masks.shape[1]):
+            ys, xs = np.where(masks[i, c])
+            if len(xs):
+                out[i, c] = (xs.min(), ys.min(), xs.max(), ys.max())
+    return out
+
+
+@pytest.mark.parametrize("kind", [None, "u8", "bits"])
+def test_mask_boxes_match_numpy(kind):
+    """Device per-(image, field) boxes (unet_forward_boxes) == np.where min/max of the masks the
+    same forward produced (inference.py:84-90), with and without caller mask buffers; empty
+    masks (torch_default weights: logits ~ -4) give -1s; W = 48 exercises a 16-bit word row."""
+    cases = [(syn.make_state_dict(0, 3, 3, "pretrained"), syn.invoice_pages(1000, 2, 512, 512, 3)),
+             (syn.make_state_dict(1, 3, 3, "torch_default"), syn.invoice_pages(2, 1, 64, 64, 3)),
+             (syn.make_state_dict(5, 3, 3, "structured", out_bias=0.0), syn.uniform_batch(3, 3, 3, 32, 48))]
+    for sd, x in cases:
+        m = make_model(sd, 3, "bf16")
+        xd = torch.from_numpy(x).to(DEV)
+        with torch.no_grad():
+            ref_masks = m.forward_masks(xd).cpu().numpy().astype(bool)
+            got = m.forward_boxes(xd, masks=kind)
+        boxes = (got if kind is None else got[1]).cpu().numpy()
+        assert np.array_equal(boxes, _np_boxes(ref_masks))
+        if kind is not None:
+            mk = got[0].cpu().numpy()
+            if kind == "bits":
+                mk = np.unpackbits(mk, axis=-1, bitorder="little")
+            assert np.array_equal(mk.astype(bool), ref_masks)
+        m.close()
+
+
+def test_config5_1024_fp16():
+    """BASELINE config 5 shape (1024x1024, 3 channels, 5 resolution levels, fp16 storage with
+    fp32 accumulation): logits vs the fp32 CPU oracle and fused masks (IoU) on one page; a
+    batch of 3 agrees with the single-image forward bitwise (no cross-image coupling)."""
+    x = syn.invoice_pages(1000, 1, 1024, 1024, 3)
+    sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
+    ref = orc.unet_forward(sd, torch.from_numpy(x)).numpy()
+    ref_masks = np.stack(list(orc.masks_from_logits(ref[0]).values()))
+    m = make_model(sd, 3, "fp16")
+    xd = torch.from_numpy(x).to(DEV)
+    with torch.no_grad():
+        masks, logits = m.forward_masks(xd, with_logits=True)
+        x3 = torch.cat([torch.from_numpy(syn.invoice_pages(7, 1, 1024, 1024, 3)).to(DEV), xd,
+                        torch.from_numpy(syn.uniform_batch(2, 1, 3, 1024, 1024)).to(DEV)])
+        lg3 = m(x3)
+    err = rel_err(logits.cpu().numpy(), ref)
+    ious = [orc.mask_iou(masks[0, k].cpu().numpy().astype(bool), ref_masks[k]) for k in range(3)]
+    print(f"1024x1024 fp16: logits rel err {err:.3e}, mask IoU {ious}")
+    assert err <= TOL["fp16"]
+    assert min(ious) >= 0.995
+    assert torch.equal(lg3[1:2], logits)
+    m.close()

@@ -41,3 +41,37 @@ def test_forward_on_cpu_fails_loudly():
 def test_bad_dtype_rejected():
     with pytest.raises(ValueError):
         UNet(3, 3, compute_dtype="int8")
+
+
+def _np_box(mask):
+    ys, xs = np.where(mask)
+    return None if len(xs) == 0 else (xs.min(), ys.min(), xs.max(), ys.max())
+
+
+def test_crops_from_boxes_equal_crops_from_masks():
+    """run_unet's crop step from device boxes (x0, y0, x1, y1 / -1s) == the reference's
+    np.where path (inference.py:84-127) on the same masks, incl. empty / 1-pixel masks."""
+    from PIL import Image
+    from unet_mi355x import inference as inf
+    rng = np.random.default_rng(0)
+    img = Image.fromarray(rng.integers(0, 256, (400, 600, 3), dtype=np.uint8), mode="RGB")
+    dark = Image.fromarray(np.zeros((300, 200, 3), dtype=np.uint8), mode="RGB")
+    for trial in range(20):
+        masks = {}
+        for i, k in enumerate(inf.FIELDS):
+            m = np.zeros((512, 512), dtype=bool)
+            kind = (trial + i) % 4
+            if kind == 1:
+                m[rng.integers(0, 512), rng.integers(0, 512)] = True
+            elif kind >= 2:
+                y0, x0 = rng.integers(0, 400, 2)
+                m[y0:y0 + rng.integers(1, 100), x0:x0 + rng.integers(1, 100)] = rng.random() < 0.9
+            masks[k] = m
+        boxes = np.array([_np_box(masks[k]) or (-1, -1, -1, -1) for k in inf.FIELDS], dtype=np.int32)
+        for pil in (img, dark):
+            a = inf.masks_to_crops(pil, masks)
+            b = inf.boxes_to_crops(pil, boxes)
+            for k in inf.FIELDS:
+                assert (a[k] is None) == (b[k] is None), (trial, k)
+                if a[k] is not None:
+                    assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]))

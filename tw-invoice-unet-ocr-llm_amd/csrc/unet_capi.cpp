@@ -76,7 +76,7 @@ struct Layer {
 };
 
 struct Buffers {
-  size_t tA, cat1, cat2, cat3, cat4, p1, p2, p3, p4, bnb, tB, total;  // byte offsets
+  size_t tA, cat1, cat2, cat3, cat4, p1, p2, p3, p4, bnb, tB, mbits, total;  // byte offsets
 };
 
 }  // namespace
@@ -151,6 +151,8 @@ Buffers plan(DType dt, int N, int H, int W) {
   b.p4 = take(P / 256 * 512);
   b.bnb = take(P / 256 * 1024);
   b.tB = take(P / 4 * 128);
+  b.mbits = o;   // bit-packed masks for unet_forward_boxes without caller masks (<= kMaxClasses fields)
+  o = align256(o + (size_t)kMaxClasses * P / 8);
   b.total = o;
   return b;
 }
@@ -296,8 +298,8 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
   if (cfg >= CFG_COUNT) {
     std::snprintf(buf, sizeof buf, "ablation_%d<%s, %d>", cfg - CFG_COUNT, tname(t), epi);
   } else if (cfg_is_ring(cfg)) {
-    const int tc = cfg_rows(cfg) / 16, ns = (cfg == CFG_RING_R128_NS3) ? 3 : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
-    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d>", tname(t), tc, ns, epi);
+    const int tc = cfg_rows(cfg) / 16;
+    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, 0>", tname(t), tc, ring_ns(cfg), epi);
   } else if (cfg_is_halo(cfg)) {
     const auto& c = halo[cfg - CFG_HALO_R128_W4];
     const int hsrc = (cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8) ? 1 : 0;
@@ -629,7 +631,7 @@ namespace {
 // The launch sequence of UNet.forward (unet_model.py:55-86).  ev (optional, kLaunches+1
 // events) brackets every launch for per-layer timing.
 int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
-                 int mask_kind, int N, int H, int W, void* stream, hipEvent_t* ev) {
+                 int mask_kind, int32_t* boxes, int N, int H, int W, void* stream, hipEvent_t* ev) {
   if (!h || !x) return fail(UNET_EINVAL, "null argument");
   if (!h->loaded) return fail(UNET_ESTATE, "weights not loaded");
   if (x_layout != UNET_LAYOUT_NCHW || x_dtype != UNET_IN_F32)
@@ -645,6 +647,10 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   const Buffers B = plan(h->dt, N, H, W);
   char* ws = h->ws;
   auto buf = [&](size_t off) { return static_cast<void*>(ws + off); };
+  if (boxes && (!masks || mask_kind == UNET_MASK_NONE)) {   // boxes only: bit masks into the workspace
+    masks = buf(B.mbits);
+    mask_kind = UNET_MASK_BITS;
+  }
   const int H2 = H / 2, W2 = W / 2, H4 = H / 4, W4 = W / 4, H8 = H / 8, W8 = W / 8, H16 = H / 16, W16 = W / 16;
 
   // down1.net.0 (C -> 64): direct conv
@@ -693,6 +699,11 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   RUN(h, h->L[C1B], EPI_HEAD, buf(B.tA), N, H, W, 64, nullptr, 0, 0, nullptr, 0, s,
       static_cast<float*>(logits), masks, mask_kind);
 #undef RUN
+  if (boxes) {   // per-(image, field) mask bounding boxes (inference.py:84-90)
+    hipError_t e = launch_mask_boxes(static_cast<const uint8_t*>(masks), mask_kind, N, h->cfg.n_classes, H, W,
+                                     boxes, s);
+    if (e != hipSuccess) return fail(UNET_EHIP, std::string("mask boxes launch: ") + hipGetErrorString(e));
+  }
   mark();
   h->lastN = N; h->lastH = H; h->lastW = W;
   return UNET_OK;
@@ -701,7 +712,13 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
 
 int unet_forward(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
                  int mask_kind, int N, int H, int W, void* stream) {
-  return forward_impl(h, x, x_layout, x_dtype, logits, masks, mask_kind, N, H, W, stream, nullptr);
+  return forward_impl(h, x, x_layout, x_dtype, logits, masks, mask_kind, nullptr, N, H, W, stream, nullptr);
+}
+
+int unet_forward_boxes(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
+                       int mask_kind, int32_t* boxes, int N, int H, int W, void* stream) {
+  if (!boxes) return fail(UNET_EINVAL, "boxes is NULL");
+  return forward_impl(h, x, x_layout, x_dtype, logits, masks, mask_kind, boxes, N, H, W, stream, nullptr);
 }
 
 int unet_num_launches(void) { return UNET_NUM_LAUNCHES; }
@@ -717,7 +734,7 @@ int unet_forward_timed(unet_handle* h, const void* x, int x_layout, int x_dtype,
   DeviceGuard g(h->cfg.device);
   hipEvent_t ev[UNET_NUM_LAUNCHES + 1];
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
-  int rc = forward_impl(h, x, x_layout, x_dtype, logits, masks, mask_kind, N, H, W, stream, ev);
+  int rc = forward_impl(h, x, x_layout, x_dtype, logits, masks, mask_kind, nullptr, N, H, W, stream, ev);
   if (!rc) {
     HIP_TRY(hipEventSynchronize(ev[UNET_NUM_LAUNCHES]));
     for (int i = 0; i < UNET_NUM_LAUNCHES; ++i) HIP_TRY(hipEventElapsedTime(&launch_ms[i], ev[i], ev[i + 1]));

@@ -82,12 +82,19 @@ enum Cfg : int {
   CFG_T8_HALO1_R64_W4 = 18, CFG_T8_HALO_R64_W4 = 19, CFG_T8_HALO_R64_W2 = 20,
   // persistent, 3-deep halo ring (two chunks / tiles of HBM loads in flight per CU)
   CFG_HALO3_R64_W8 = 21, CFG_HALO3_R64_W4 = 22,
-  CFG_COUNT = 23
+  // single halo buffer with the fixed read/MFMA interleave (PIPE 7, sched_group_barrier)
+  CFG_SG_R128T8_NS2 = 23, CFG_SG_R128T8_NS3 = 24, CFG_SG_R64_W4 = 25, CFG_SG_R64_W8 = 26,
+  // 32-channel (64-byte-row) K chunks: double-buffered halo + NS-slot weight ring, persistent,
+  // weights pre-packed in step order per row tile (a different K order: chunk32-major, tap-minor)
+  CFG_RING_R128 = 27, CFG_RING_R64 = 28, CFG_RING_R128_NS3 = 29, CFG_RING_R64_NS5 = 30,
+  CFG_COUNT = 31
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);
 int cfg_pixels(int cfg);
 bool cfg_is_halo(int cfg);
+bool cfg_is_ring(int cfg);   // 64-byte-row ring kernel: step-major packed weights
+int ring_ns(int cfg);       // ring kernel: weight-ring slots
 int cfg_limit();   // number of valid Cfg values in this build
 
 hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s);
@@ -95,5 +102,9 @@ hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s);
 // NHWC (pixel stride ld, channel offset choff, C channels) element type t -> NCHW fp32
 hipError_t launch_nhwc_to_nchw_f32(DType t, const void* src, int N, int H, int W, int C, int ld,
                                    int choff, float* dst, hipStream_t s);
+// per-(image, field) mask bounding boxes [N*ncls][4] = x_min, y_min, x_max, y_max (-1s if empty)
+constexpr int kMaxBoxW = 16384;
+hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, int H, int W, int* boxes,
+                             hipStream_t s);
 
 }  // namespace unet

@@ -46,6 +46,7 @@ int cfg_pixels(int cfg) {
 }
 bool cfg_is_halo(int cfg) { return cfg >= CFG_HALO_R128_W4; }
 bool cfg_is_ring(int cfg) { return cfg >= CFG_RING_R128 && cfg <= CFG_RING_R64_NS5; }
+int ring_ns(int cfg) { return cfg == CFG_RING_R128_NS3 ? 3 : (cfg == CFG_RING_R64_NS5 ? 5 : 4); }
 int cfg_limit() {
 #ifdef UNET_ABLATION
   return CFG_COUNT + 15;
@@ -1388,6 +1389,74 @@ hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s) {
     case DType::F16: return first_t<_Float16>(a, s);
   }
   return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------------
+// per-(image, field) bounding box of a mask: inference.py:84-90 (np.where(mask) ->
+// xs.min(), xs.max(), ys.min(), ys.max()) on the GPU, 4 ints instead of H*W host bytes.
+// One block per (n, c).  Bit-packed masks are read as little-endian 16-bit words (bit j of
+// word w = pixel 16*w + j; W % 16 == 0); each thread ORs its words into a per-block column
+// mask in LDS and keeps the first / last row with a set bit.  Empty mask -> (-1,-1,-1,-1).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mask_boxes_kernel(const uint8_t* __restrict__ masks, int kind, int H, int W,
+                                                        int* __restrict__ boxes) {
+  __shared__ unsigned col_or[kMaxBoxW / 16];
+  __shared__ int ymin_s, ymax_s, xmin_s, xmax_s;
+  const int tid = threadIdx.x;
+  const int words = W / 16;
+  for (int i = tid; i < words; i += 256) col_or[i] = 0u;
+  if (tid == 0) { ymin_s = 0x7FFFFFFF; ymax_s = -1; xmin_s = 0x7FFFFFFF; xmax_s = -1; }
+  __syncthreads();
+  int ymin = 0x7FFFFFFF, ymax = -1;
+  if (kind == MASK_BITS) {
+    const uint16_t* m = reinterpret_cast<const uint16_t*>(masks) + (size_t)blockIdx.x * H * words;
+    const int total = H * words;
+    for (int i = tid; i < total; i += 256) {
+      const unsigned v = m[i];
+      if (v) {
+        const int y = i / words;
+        ymin = min(ymin, y);
+        ymax = max(ymax, y);
+        atomicOr(&col_or[i - y * words], v);
+      }
+    }
+  } else {
+    const uint8_t* m = masks + (size_t)blockIdx.x * H * W;
+    const int total = H * W;
+    for (int i = tid; i < total; i += 256) {
+      if (m[i]) {
+        const int y = i / W, x = i - y * W;
+        ymin = min(ymin, y);
+        ymax = max(ymax, y);
+        atomicOr(&col_or[x >> 4], 1u << (x & 15));
+      }
+    }
+  }
+  if (ymax >= 0) { atomicMin(&ymin_s, ymin); atomicMax(&ymax_s, ymax); }
+  __syncthreads();
+  for (int i = tid; i < words; i += 256) {
+    const unsigned v = col_or[i];
+    if (v) {
+      atomicMin(&xmin_s, 16 * i + __builtin_ctz(v));
+      atomicMax(&xmax_s, 16 * i + 31 - __builtin_clz(v));
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int* b = boxes + (size_t)blockIdx.x * 4;
+    const bool any = ymax_s >= 0;
+    b[0] = any ? xmin_s : -1;
+    b[1] = any ? ymin_s : -1;
+    b[2] = any ? xmax_s : -1;
+    b[3] = any ? ymax_s : -1;
+  }
+}
+
+hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, int H, int W, int* boxes,
+                             hipStream_t s) {
+  if (W % 16 || W > kMaxBoxW || (kind != MASK_BITS && kind != MASK_U8)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mask_boxes_kernel, dim3((unsigned)(N * ncls)), dim3(256), 0, s, masks, kind, H, W, boxes);
+  return hipGetLastError();
 }
 
 template <typename T>

@@ -6,7 +6,9 @@ Differences are internal only:
   * the model is cached per (checkpoint, mtime, device) instead of re-loaded on every
     call (the reference re-reads the 124 MB checkpoint per call, inference.py:58);
   * sigmoid + thresholds run fused in the native head kernel (masks come back as
-    uint8), so the 3x512x512 fp32 probability map never leaves the GPU.
+    uint8), so the 3x512x512 fp32 probability map never leaves the GPU;
+  * the per-field bounding boxes (np.where -> min/max, inference.py:84-90) are computed
+    on the GPU too (unet_forward_boxes); the scale / 15 % pad / crop stays on the host.
 """
 from __future__ import annotations
 
@@ -63,6 +65,35 @@ def preprocess(pil_img: Image.Image) -> torch.Tensor:
     return torch.from_numpy(preprocess_array(pil_img)).unsqueeze(0).to(DEVICE)
 
 
+def crop_from_box(pil_img: Image.Image, box):
+    """inference.py:92-127 for one field: mask-space box (x_min, y_min, x_max, y_max), or None
+    for an empty mask -> original scale -> 15% pad -> clamp -> crop, rejecting degenerate and
+    near-black crops (None)."""
+    if box is None:
+        return None
+    mx1, my1, mx2, my2 = (int(v) for v in box)
+    ow, oh = pil_img.size
+    scale_x, scale_y = ow / IMG_SIZE, oh / IMG_SIZE
+    x1, x2 = int(mx1 * scale_x), int(mx2 * scale_x)
+    y1, y2 = int(my1 * scale_y), int(my2 * scale_y)
+    pad_x, pad_y = int((x2 - x1) * CROP_PAD), int((y2 - y1) * CROP_PAD)
+    x1, y1 = max(0, x1 - pad_x), max(0, y1 - pad_y)
+    x2, y2 = min(ow, x2 + pad_x), min(oh, y2 + pad_y)
+    if x2 <= x1 or y2 <= y1:
+        return None
+    crop = pil_img.crop((x1, y1, x2, y2))
+    arr = np.array(crop)
+    if arr.size == 0 or arr.mean() < 3:
+        return None
+    return crop
+
+
+def boxes_to_crops(pil_img: Image.Image, boxes) -> dict:
+    """Crops from device-computed mask boxes (int32 [n_fields, 4], -1s = empty mask)."""
+    b = np.asarray(boxes)
+    return {k: crop_from_box(pil_img, None if b[i, 2] < 0 else b[i]) for i, k in enumerate(FIELDS)}
+
+
 def masks_to_crops(pil_img: Image.Image, masks: dict) -> dict:
     """inference.py:84-127: bbox per mask -> original scale -> 15% pad -> crop, rejecting
     empty / degenerate / near-black crops (None)."""
@@ -98,7 +129,8 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
     model = _cached_model(checkpoint_path, compute_dtype)
     img_resized = pil_img.resize((IMG_SIZE, IMG_SIZE))            # inference.py:63
     x = preprocess(img_resized)                                    # inference.py:64
-    with torch.no_grad():
-        m = model.forward_masks(x)[0].cpu().numpy().astype(bool)   # fused sigmoid+threshold
+    with torch.no_grad():   # fused sigmoid + threshold + per-field bounding boxes on the device
+        m, boxes = model.forward_boxes(x, masks="u8")
+    m = m[0].cpu().numpy().astype(bool)
     masks = {k: m[i] for i, k in enumerate(FIELDS)}
-    return masks, masks_to_crops(pil_img, masks)
+    return masks, boxes_to_crops(pil_img, boxes[0].cpu().numpy())

@@ -115,7 +115,7 @@ class UNet(nn.Module):
             # the reference fails inside torch.cat for such sizes
             raise RuntimeError(f"UNet input H and W must be divisible by 16, got {tuple(x.shape[2:])}")
 
-    def _run(self, x: torch.Tensor, want_logits: bool, mask_kind: int):
+    def _run(self, x: torch.Tensor, want_logits: bool, mask_kind: int, want_boxes: bool = False):
         self._check_input(x)
         h = self.native_handle(x.device)
         x = x.detach()
@@ -130,8 +130,15 @@ class UNet(nn.Module):
         elif mask_kind == native.MASK_BITS:
             masks = torch.empty((n, self.n_classes, hh, ww // 8), device=x.device, dtype=torch.uint8)
         stream = torch.cuda.current_stream(x.device).cuda_stream
+        boxes = None
         with torch.cuda.device(x.device):
-            h.forward(x, logits, masks, mask_kind, stream)
+            if want_boxes:
+                boxes = torch.empty((n, self.n_classes, 4), device=x.device, dtype=torch.int32)
+                h.forward_boxes(x, logits, masks, mask_kind, boxes, stream)
+            else:
+                h.forward(x, logits, masks, mask_kind, stream)
+        if want_boxes:
+            return logits, masks, boxes
         return logits, masks
 
     # ------------------------------------------------------------------ public API
@@ -148,6 +155,17 @@ class UNet(nn.Module):
         """
         logits, masks = self._run(x, with_logits, native.MASK_BITS if packed else native.MASK_U8)
         return (masks, logits) if with_logits else masks
+
+    def forward_boxes(self, x: torch.Tensor, masks: str | None = None):
+        """Fused masks + per-(image, field) bounding boxes on the device (inference.py:72-90).
+
+        Returns int32 boxes [N, n_classes, 4] = (x_min, y_min, x_max, y_max) in mask pixels,
+        inclusive, (-1, -1, -1, -1) for an empty mask -- the np.where -> min/max of run_unet.
+        ``masks`` = None (boxes only), "u8" or "bits": also return that mask tensor first.
+        """
+        kind = {None: native.MASK_NONE, "u8": native.MASK_U8, "bits": native.MASK_BITS}[masks]
+        _, m, boxes = self._run(x, False, kind, want_boxes=True)
+        return boxes if masks is None else (m, boxes)
 
     def reserve(self, n: int, h: int, w: int, device=None) -> None:
         """Pre-allocate the native workspace (so forwards do not allocate)."""

@@ -42,6 +42,7 @@ SIGNATURES = {
     "unet_workspace_bytes": (_sz, [_vp, _i, _i, _i]),
     "unet_reserve": (_i, [_vp, _i, _i, _i]),
     "unet_forward": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp]),
+    "unet_forward_boxes": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _i, _vp]),
     "unet_num_launches": (_i, []),
     "unet_launch_label": (ctypes.c_char_p, [_vp, _i]),
     "unet_forward_timed": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
@@ -138,6 +139,18 @@ class Handle:
                                         None if logits is None else logits.data_ptr(),
                                         None if masks is None else masks.data_ptr(),
                                         mask_kind, n, h, w, stream), "unet_forward")
+
+    def forward_boxes(self, x: torch.Tensor, logits: torch.Tensor | None, masks: torch.Tensor | None,
+                      mask_kind: int, boxes: torch.Tensor, stream: int) -> None:
+        """forward + per-(image, field) mask boxes: int32 [N][n_classes][4] = x0, y0, x1, y1 (-1s if empty)."""
+        n, c, h, w = x.shape
+        if boxes.dtype != torch.int32 or tuple(boxes.shape) != (n, self.n_classes, 4) or not boxes.is_contiguous():
+            raise ValueError(f"boxes must be a contiguous int32 tensor of shape {(n, self.n_classes, 4)}")
+        with self.lock:
+            check(self.lib.unet_forward_boxes(self._h, x.data_ptr(), LAYOUT_NCHW, IN_F32,
+                                              None if logits is None else logits.data_ptr(),
+                                              None if masks is None else masks.data_ptr(),
+                                              mask_kind, boxes.data_ptr(), n, h, w, stream), "unet_forward_boxes")
 
     def forward_timed(self, x: torch.Tensor, logits: torch.Tensor | None, masks: torch.Tensor | None,
                       mask_kind: int, stream: int) -> list:
