@@ -10,6 +10,8 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 echo tests ok
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 echo bench ok
+timeout -k 10 300 python bench.py --size 1024 --batch 64 --dtype fp16 --steps 3 --cpu-seconds 10 > gpurun_out/bench_${TAG}_cfg5_fp16_1024.json 2> gpurun_out/bench_${TAG}_cfg5.err
+echo bench cfg5 ok
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_$TAG.err
 echo prof ok

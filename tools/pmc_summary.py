@@ -69,7 +69,7 @@ def main():
             continue
         rows = load_pass(p)
         ours = [(did, v) for did, v in sorted(rows.items())
-                if "igemm" in v[0] or "first_conv" in v[0] or "halo" in v[0]]
+                if any(s in v[0] for s in ("igemm", "first_conv", "halo", "ring_kernel"))]
         last = ours[-len(launches):]
         for i, (did, (name, ctr)) in enumerate(last):
             per_launch[i].update(ctr)
