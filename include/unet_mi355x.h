@@ -109,6 +109,16 @@ int unet_forward_boxes(unet_handle* h, const void* x, int x_layout, int x_dtype,
                        void* logits, void* masks, int mask_kind, int32_t* boxes,
                        int N, int H, int W, void* hip_stream);
 
+/* GPU preprocessing of one photo (inference.py:62-64 + preprocess, :30-44):
+ * PIL Image.resize((ow, oh)) with Pillow's default BICUBIC filter -- bit-exact with Pillow's
+ * fixed-point separable resampler --, convert("RGB") (gray replicated), /255 as float32, CHW.
+ * img: device uint8 HWC [ih][iw][channels], channels 3 (mode "RGB") or 1 (mode "L");
+ * x:   device fp32 [3][oh][ow] (e.g. one image's slot of the unet_forward input batch).
+ * Coefficient tables are cached per (ih, iw, oh, ow) in the handle (first call per geometry
+ * uploads them synchronously).  Stream-ordered on hip_stream. */
+int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channels,
+                    float* x, int oh, int ow, void* hip_stream);
+
 /* Number of kernel launches in one forward (first conv, 17 implicit-GEMM 3x3 convs with
  * the fused pool / head epilogues, 4 ConvTranspose2d), in execution order:
  * down1.0 down1.3 down2.0 down2.3 down3.0 down3.3 down4.0 down4.3 bottleneck.0

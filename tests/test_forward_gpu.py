@@ -339,3 +339,27 @@ def test_config5_1024_fp16():
     assert min(ious) >= 0.995
     assert torch.equal(lg3[1:2], logits)
     m.close()
+
+
+@pytest.mark.parametrize("h,w,c", [(400, 600, 3), (1333, 1000, 3), (200, 300, 3), (700, 512, 3),
+                                   (512, 900, 3), (512, 512, 3), (390, 517, 1), (37, 23, 3), (3024, 4032, 3)])
+def test_preprocess_bit_exact_with_pillow(h, w, c):
+    """unet_preprocess (GPU) == PIL Image.resize((512, 512)) (default BICUBIC) + convert("RGB")
+    + /255, bit for bit: down / up / one-axis / identity geometries, RGB and L, a 12 MP photo."""
+    from PIL import Image
+    rng = np.random.default_rng(h + 3 * w)
+    arr = rng.integers(0, 256, (h, w, c) if c == 3 else (h, w), dtype=np.uint8)
+    if h == 3024:   # smooth photo-like content (strong low-pass response, clip8 at both ends)
+        yy, xx = np.mgrid[0:h, 0:w]
+        arr = (127.5 + 127.5 * (np.sin(yy / 37.0) * np.cos(xx / 53.0))[..., None] + rng.normal(0, 20, (h, w, 3))
+               ).clip(0, 255).astype(np.uint8)
+    pil = Image.fromarray(arr)
+    ref = np.array(pil.resize((512, 512)).convert("RGB")).astype(np.float32) / 255.0
+    m = make_model(syn.make_state_dict(0, 3, 3), 3, "bf16")
+    got = m.preprocess(torch.from_numpy(arr).to(DEV)).cpu().numpy()[0]
+    assert got.shape == (3, 512, 512)
+    assert np.array_equal(got, ref.transpose(2, 0, 1))
+    if h < 2000:   # the numpy restatement agrees too (checker of the checker)
+        from oracle import pil_resample as pr
+        assert np.array_equal(got, pr.to_input(arr))
+    m.close()

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <tuple>
 #include <vector>
 
 using namespace unet;
@@ -75,6 +76,12 @@ struct Layer {
   float* b = nullptr;  // [ctot] natural order
 };
 
+// Device coefficient tables of one resize geometry (unet_preprocess), owned by the handle.
+struct ResampleStore {
+  ResamplePlan plan{};
+  std::vector<void*> bufs;
+};
+
 struct Buffers {
   size_t tA, cat1, cat2, cat3, cat4, p1, p2, p3, p4, bnb, tB, mbits, total;  // byte offsets
 };
@@ -97,6 +104,9 @@ struct unet_handle {
   size_t ws_bytes = 0;
   int lastN = 0, lastH = 0, lastW = 0;
   std::vector<void*> allocs;
+  std::map<std::tuple<int, int, int, int>, ResampleStore> resample;   // (ih, iw, oh, ow) -> tables
+  uint8_t* pp_tmp = nullptr;              // horizontal-pass rows of unet_preprocess
+  size_t pp_tmp_bytes = 0;
   std::string labels[UNET_NUM_LAUNCHES];   // kernel instantiation of every launch
   float thr_logit[kMaxClasses];           // per-class logit cut, see unet_logit_cut
 };
@@ -266,10 +276,63 @@ int packT(unet_handle* h, Layer& L, const float* W, const float* B) {
 void free_all(unet_handle* h) {
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
+  for (auto& kv : h->resample)
+    for (void* p : kv.second.bufs) (void)hipFree(p);
+  h->resample.clear();
+  if (h->pp_tmp) (void)hipFree(h->pp_tmp);
+  h->pp_tmp = nullptr;
+  h->pp_tmp_bytes = 0;
   if (h->ws) (void)hipFree(h->ws);
   h->ws = nullptr;
   h->ws_bytes = 0;
 }
+
+// ---- Pillow's resize coefficients (libImaging/Resample.c: precompute_coeffs +
+// normalize_coeffs_8bpc, BICUBIC a = -0.5, support 2), same double-precision operation order
+#pragma clang fp contract(off)
+double bicubic_filter(double x) {
+  const double a = -0.5;
+  if (x < 0.0) x = -x;
+  if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+  if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+  return 0.0;
+}
+
+int resample_coeffs(int in_size, int out_size, std::vector<int>& bounds, std::vector<int>& kk) {
+  const float in0 = 0.f, in1 = (float)in_size;   // Pillow's box edges are floats
+  const double scale = (double)(in1 - in0) / out_size;
+  double filterscale = scale;
+  if (filterscale < 1.0) filterscale = 1.0;
+  const double support = 2.0 * filterscale;      // antialiasing: widen by the downscale factor
+  const int ksize = (int)std::ceil(support) * 2 + 1;
+  bounds.assign((size_t)2 * out_size, 0);
+  kk.assign((size_t)out_size * ksize, 0);
+  std::vector<double> k(ksize);
+  for (int xx = 0; xx < out_size; ++xx) {
+    const double center = in0 + (xx + 0.5) * scale;
+    double ww = 0.0;
+    const double ss = 1.0 / filterscale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    for (int x = 0; x < xmax; ++x) {
+      const double w = bicubic_filter((x + xmin - center + 0.5) * ss);
+      k[x] = w;
+      ww += w;
+    }
+    for (int x = 0; x < xmax; ++x) {
+      double v = k[x];
+      if (ww != 0.0) v /= ww;
+      kk[(size_t)xx * ksize + x] = v < 0 ? (int)(-0.5 + v * (1 << 22)) : (int)(0.5 + v * (1 << 22));
+    }
+    bounds[2 * xx] = xmin;
+    bounds[2 * xx + 1] = xmax;
+  }
+  return ksize;
+}
+#pragma clang fp contract(on)
 
 int check_geometry(const unet_handle* h, int N, int H, int W) {
   if (N <= 0 || H <= 0 || W <= 0) return fail(UNET_EINVAL, "N, H, W must be positive");
@@ -719,6 +782,66 @@ int unet_forward_boxes(unet_handle* h, const void* x, int x_layout, int x_dtype,
                        int mask_kind, int32_t* boxes, int N, int H, int W, void* stream) {
   if (!boxes) return fail(UNET_EINVAL, "boxes is NULL");
   return forward_impl(h, x, x_layout, x_dtype, logits, masks, mask_kind, boxes, N, H, W, stream, nullptr);
+}
+
+int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channels, float* x, int oh, int ow,
+                    void* stream) {
+  if (!h || !img || !x) return fail(UNET_EINVAL, "null argument");
+  if (channels != 1 && channels != 3) return fail(UNET_EINVAL, "channels must be 1 (L) or 3 (RGB)");
+  if (ih <= 0 || iw <= 0 || oh <= 0 || ow <= 0 || (long long)ih * iw > (1LL << 30) || oh > 16384 || ow > 16384)
+    return fail(UNET_EINVAL, "bad image or output size");
+  DeviceGuard g(h->cfg.device);
+  const auto key = std::make_tuple(ih, iw, oh, ow);
+  auto it = h->resample.find(key);
+  if (it == h->resample.end()) {
+    ResampleStore st;
+    ResamplePlan& p = st.plan;
+    p.ih = ih; p.iw = iw; p.oh = oh; p.ow = ow;
+    p.need_h = ow != iw;
+    p.need_v = oh != ih;
+    std::vector<int> hb, hk, vb, vk;
+    p.h_ksize = resample_coeffs(iw, ow, hb, hk);
+    p.v_ksize = resample_coeffs(ih, oh, vb, vk);
+    p.h_y0 = 0;
+    p.h_rows = ih;
+    if (p.need_h && p.need_v) {   // the horizontal pass covers only the rows the vertical pass reads
+      p.h_y0 = vb[0];
+      p.h_rows = vb[2 * (oh - 1)] + vb[2 * (oh - 1) + 1] - p.h_y0;
+      for (int i = 0; i < oh; ++i) vb[2 * i] -= p.h_y0;
+    }
+    const std::vector<int>* src[4] = {&hb, &hk, &vb, &vk};
+    const int** dst[4] = {&p.h_bounds, &p.h_kk, &p.v_bounds, &p.v_kk};
+    for (int i = 0; i < 4; ++i) {
+      void* d = nullptr;
+      const size_t bytes = src[i]->size() * sizeof(int);
+      hipError_t e = hipMalloc(&d, bytes);
+      if (e != hipSuccess) {
+        for (void* q : st.bufs) (void)hipFree(q);
+        return fail(UNET_ENOMEM, std::string("resample tables: ") + hipGetErrorString(e));
+      }
+      st.bufs.push_back(d);
+      HIP_TRY(hipMemcpy(d, src[i]->data(), bytes, hipMemcpyHostToDevice));
+      *dst[i] = static_cast<const int*>(d);
+    }
+    it = h->resample.emplace(key, std::move(st)).first;
+  }
+  const ResamplePlan& p = it->second.plan;
+  const size_t tmp = p.need_h ? (size_t)p.h_rows * ow * channels : 0;
+  if (tmp > h->pp_tmp_bytes) {
+    if (h->pp_tmp) {
+      HIP_TRY(hipDeviceSynchronize());
+      (void)hipFree(h->pp_tmp);
+      h->pp_tmp = nullptr;
+      h->pp_tmp_bytes = 0;
+    }
+    hipError_t e = hipMalloc((void**)&h->pp_tmp, tmp);
+    if (e != hipSuccess) return fail(UNET_ENOMEM, std::string("preprocess buffer: ") + hipGetErrorString(e));
+    h->pp_tmp_bytes = tmp;
+  }
+  hipError_t e = launch_resample(p, static_cast<const uint8_t*>(img), channels, h->pp_tmp, x,
+                                 static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail(UNET_EHIP, std::string("resample launch: ") + hipGetErrorString(e));
+  return UNET_OK;
 }
 
 int unet_num_launches(void) { return UNET_NUM_LAUNCHES; }

@@ -102,6 +102,20 @@ hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s);
 // NHWC (pixel stride ld, channel offset choff, C channels) element type t -> NCHW fp32
 hipError_t launch_nhwc_to_nchw_f32(DType t, const void* src, int N, int H, int W, int C, int ld,
                                    int choff, float* dst, hipStream_t s);
+// Pillow-exact separable resize (unet_preprocess.hip): device coefficient tables of one
+// (ih, iw) -> (oh, ow) geometry.  bounds: [out][2] = (first input index, taps); kk: [out][ksize]
+// int32 fixed-point weights (22 fractional bits).  The vertical bounds are relative to h_y0
+// when the horizontal pass runs (it produces only rows h_y0 .. h_y0 + h_rows - 1).
+struct ResamplePlan {
+  int ih, iw, oh, ow;
+  bool need_h, need_v;
+  int h_y0, h_rows, h_ksize, v_ksize;
+  const int* h_bounds; const int* h_kk;
+  const int* v_bounds; const int* v_kk;
+};
+hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int C, uint8_t* tmp, float* out,
+                           hipStream_t s);
+
 // per-(image, field) mask bounding boxes [N*ncls][4] = x_min, y_min, x_max, y_max (-1s if empty)
 constexpr int kMaxBoxW = 16384;
 hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, int H, int W, int* boxes,

@@ -8,7 +8,9 @@ Differences are internal only:
   * sigmoid + thresholds run fused in the native head kernel (masks come back as
     uint8), so the 3x512x512 fp32 probability map never leaves the GPU;
   * the per-field bounding boxes (np.where -> min/max, inference.py:84-90) are computed
-    on the GPU too (unet_forward_boxes); the scale / 15 % pad / crop stays on the host.
+    on the GPU too (unet_forward_boxes); the scale / 15 % pad / crop stays on the host;
+  * RGB / L photos are resized on the GPU (unet_preprocess, bit-exact with Pillow's
+    BICUBIC resize), so only the original uint8 photo crosses PCIe.
 """
 from __future__ import annotations
 
@@ -127,8 +129,12 @@ def masks_to_crops(pil_img: Image.Image, masks: dict) -> dict:
 def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | None = None):
     """inference.py:50-129 -> (masks: {field: bool[512,512]}, crops: {field: PIL.Image | None})."""
     model = _cached_model(checkpoint_path, compute_dtype)
-    img_resized = pil_img.resize((IMG_SIZE, IMG_SIZE))            # inference.py:63
-    x = preprocess(img_resized)                                    # inference.py:64
+    if pil_img.mode in ("RGB", "L") and str(DEVICE).startswith("cuda"):
+        # inference.py:63-64 on the GPU: Pillow-exact BICUBIC resize + convert("RGB") + /255
+        img = torch.from_numpy(np.ascontiguousarray(np.asarray(pil_img))).to(DEVICE)
+        x = model.preprocess(img, IMG_SIZE)
+    else:   # other PIL modes (RGBA premultiplied resize, P nearest, ...): the reference's host path
+        x = preprocess(pil_img.resize((IMG_SIZE, IMG_SIZE)))      # inference.py:63-64
     with torch.no_grad():   # fused sigmoid + threshold + per-field bounding boxes on the device
         m, boxes = model.forward_boxes(x, masks="u8")
     m = m[0].cpu().numpy().astype(bool)

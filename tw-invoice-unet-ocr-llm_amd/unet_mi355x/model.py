@@ -167,6 +167,23 @@ class UNet(nn.Module):
         _, m, boxes = self._run(x, False, kind, want_boxes=True)
         return boxes if masks is None else (m, boxes)
 
+    def preprocess(self, img: torch.Tensor, size: int = 512, out: torch.Tensor | None = None) -> torch.Tensor:
+        """inference.py:62-64 + :30-44 on the device: a photo as uint8 [H, W, 3] (RGB) or
+        [H, W] / [H, W, 1] (L) device tensor -> fp32 [1, 3, size, size] network input, with
+        Pillow's default BICUBIC resize reproduced bit-exactly (csrc/unet_preprocess.hip).
+        ``out`` (optional, fp32 [3, size, size] contiguous, e.g. a slot of a batch) is filled
+        in place."""
+        if img.dim() == 2:
+            img = img.unsqueeze(-1)
+        if img.device.type != "cuda":
+            raise RuntimeError("unet_mi355x: preprocess runs on a ROCm GPU tensor; there is no CPU fallback")
+        img = img.contiguous()
+        h = self.native_handle(img.device)
+        dst = out if out is not None else torch.empty((3, size, size), device=img.device, dtype=torch.float32)
+        with torch.cuda.device(img.device):
+            h.preprocess(img, dst, torch.cuda.current_stream(img.device).cuda_stream)
+        return dst.unsqueeze(0) if out is None else out
+
     def reserve(self, n: int, h: int, w: int, device=None) -> None:
         """Pre-allocate the native workspace (so forwards do not allocate)."""
         dev = torch.device(device) if device is not None else next(self.parameters()).device

@@ -43,6 +43,7 @@ SIGNATURES = {
     "unet_reserve": (_i, [_vp, _i, _i, _i]),
     "unet_forward": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp]),
     "unet_forward_boxes": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _i, _vp]),
+    "unet_preprocess": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _i, _vp]),
     "unet_num_launches": (_i, []),
     "unet_launch_label": (ctypes.c_char_p, [_vp, _i]),
     "unet_forward_timed": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
@@ -151,6 +152,17 @@ class Handle:
                                               None if logits is None else logits.data_ptr(),
                                               None if masks is None else masks.data_ptr(),
                                               mask_kind, boxes.data_ptr(), n, h, w, stream), "unet_forward_boxes")
+
+    def preprocess(self, img: torch.Tensor, out: torch.Tensor, stream: int) -> None:
+        """uint8 HWC image (device) -> fp32 [3, oh, ow] (device, ``out``): Pillow-exact resize + /255."""
+        if img.dtype != torch.uint8 or img.dim() != 3 or not img.is_contiguous():
+            raise ValueError("img must be a contiguous uint8 [H, W, C] device tensor")
+        if out.dtype != torch.float32 or out.dim() != 3 or out.shape[0] != 3 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous float32 [3, oh, ow] device tensor")
+        ih, iw, c = img.shape
+        with self.lock:
+            check(self.lib.unet_preprocess(self._h, img.data_ptr(), ih, iw, c, out.data_ptr(),
+                                           out.shape[1], out.shape[2], stream), "unet_preprocess")
 
     def forward_timed(self, x: torch.Tensor, logits: torch.Tensor | None, masks: torch.Tensor | None,
                       mask_kind: int, stream: int) -> list:
