@@ -362,7 +362,8 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
     std::snprintf(buf, sizeof buf, "ablation_%d<%s, %d>", cfg - CFG_COUNT, tname(t), epi);
   } else if (cfg_is_ring(cfg)) {
     const int tc = cfg_rows(cfg) / 16;
-    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, 0>", tname(t), tc, ring_ns(cfg), epi);
+    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, 0, %d>", tname(t), tc, ring_ns(cfg), epi,
+                  ring_tps(cfg));
   } else if (cfg_is_halo(cfg)) {
     const auto& c = halo[cfg - CFG_HALO_R128_W4];
     const int hsrc = (cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8) ? 1 : 0;

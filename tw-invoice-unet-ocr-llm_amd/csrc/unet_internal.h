@@ -87,7 +87,9 @@ enum Cfg : int {
   // 32-channel (64-byte-row) K chunks: double-buffered halo + NS-slot weight ring, persistent,
   // weights pre-packed in step order per row tile (a different K order: chunk32-major, tap-minor)
   CFG_RING_R128 = 27, CFG_RING_R64 = 28, CFG_RING_R128_NS3 = 29, CFG_RING_R64_NS5 = 30,
-  CFG_COUNT = 31
+  // 64-row ring stepping one kernel row (3 taps, 48 MFMAs per wave) per barrier, 3 slots of 3 taps
+  CFG_RING_R64_T3 = 31,
+  CFG_COUNT = 32
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);
@@ -95,6 +97,7 @@ int cfg_pixels(int cfg);
 bool cfg_is_halo(int cfg);
 bool cfg_is_ring(int cfg);   // 64-byte-row ring kernel: step-major packed weights
 int ring_ns(int cfg);       // ring kernel: weight-ring slots
+int ring_tps(int cfg);      // ring kernel: taps per step
 int cfg_limit();   // number of valid Cfg values in this build
 
 hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s);

@@ -45,8 +45,11 @@ int cfg_pixels(int cfg) {
           cfg == CFG_T8_HALO_R64_W2) ? 128 : 256;
 }
 bool cfg_is_halo(int cfg) { return cfg >= CFG_HALO_R128_W4; }
-bool cfg_is_ring(int cfg) { return cfg >= CFG_RING_R128 && cfg <= CFG_RING_R64_NS5; }
-int ring_ns(int cfg) { return cfg == CFG_RING_R128_NS3 ? 3 : (cfg == CFG_RING_R64_NS5 ? 5 : 4); }
+bool cfg_is_ring(int cfg) { return cfg >= CFG_RING_R128 && cfg <= CFG_RING_R64_T3; }
+int ring_ns(int cfg) {
+  return (cfg == CFG_RING_R128_NS3 || cfg == CFG_RING_R64_T3) ? 3 : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
+}
+int ring_tps(int cfg) { return cfg == CFG_RING_R64_T3 ? 3 : 1; }
 int cfg_limit() {
 #ifdef UNET_ABLATION
   return CFG_COUNT + 15;
@@ -876,7 +879,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
 // overlaps the loads of the next.
 constexpr int kRingPix = 18 * 18;
 
-template <typename T, int WR, int WPX, int TCW, int NS>
+template <typename T, int WR, int WPX, int TCW, int NS, int TPS = 1>
 struct RingGeom {
   static constexpr int NW = WR * WPX;
   static constexpr int TC = TCW;
@@ -888,9 +891,10 @@ struct RingGeom {
   static constexpr int HI = (kRingPix + RPI * HLW - 1) / (RPI * HLW);
   static constexpr int HALO_BYTES = HI * HLW * RPI * 64;
   static constexpr int WI = BR / (RPI * NW);
-  static constexpr int WSLOT = BR * 64;
+  static constexpr int WSLOT = BR * 64;              // one tap's weights
+  static constexpr int SLOT = TPS * WSLOT;           // one ring slot = one step = TPS taps
   static constexpr int WOFF = 2 * HALO_BYTES;
-  static constexpr int PARAM_OFF = WOFF + NS * WSLOT;
+  static constexpr int PARAM_OFF = WOFF + NS * SLOT;
   static constexpr int LDS_BYTES = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
   static constexpr int BLOCKS_PER_CU = (160 * 1024) / LDS_BYTES;
 };
@@ -916,12 +920,17 @@ __device__ __forceinline__ void ring_wait(int nw, bool halo) {
   if (halo) wait_vm_barrier<HI>(); else wait_vm_barrier<0>();
 }
 
-template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0>
+// TPS = taps per step (1, or 3 = one kernel row): a step then runs TPS x TC x TP MFMAs per wave
+// between barriers and its ring slot holds TPS taps of weights (contiguous in the step-order
+// packing, so the pack is the same).
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0, int TPS = 1>
 __global__ __launch_bounds__(64 * WR * WPX, 2) void conv3x3_ring_kernel(const IgemmArgs a) {
-  using G = RingGeom<T, WR, WPX, TCW, NS>;
+  using G = RingGeom<T, WR, WPX, TCW, NS, TPS>;
   constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
   constexpr int HI = G::HI, WI = G::WI, HLW = G::HLW, HALO_BYTES = G::HALO_BYTES, WSLOT = G::WSLOT;
-  constexpr int WOFF = G::WOFF;
+  constexpr int WOFF = G::WOFF, SLOT = G::SLOT;
+  constexpr int SPC = 9 / TPS;   // steps per 32-channel chunk
+  static_assert(TPS == 1 || TPS == 3, "taps per step");
   static_assert(NS >= 3 && NS <= 5, "weight ring depth");
   static_assert(WI >= 1 && BR % (G::RPI * NW) == 0, "weight tile split");
   static_assert(TP >= 1 && 16 % WPX == 0, "pixel groups per wave");
@@ -952,13 +961,13 @@ __global__ __launch_bounds__(64 * WR * WPX, 2) void conv3x3_ring_kernel(const Ig
 
   const int H = a.H, W = a.W;
   const int nch = a.Cin / BKE;
-  const int S = 9 * nch;
+  const int S = SPC * nch;
   const int total = items * S;
   const int hseq_end = items * nch;
 
   // weights of row tile ct in step order: step s at wblk + s * WSLOT; per lane one 16-byte
   // chunk of row (wave*WI + j)*16 + lane/4, stored at position lane&3 = chunk ^ ((row>>1)&3)
-  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * WSLOT +
+  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * SLOT +
                      (wave * WI * 16 + (lane >> 2)) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
   const char* in = reinterpret_cast<const char*>(a.in);
   const char* zero = reinterpret_cast<const char*>(a.zero);
@@ -992,10 +1001,12 @@ __global__ __launch_bounds__(64 * WR * WPX, 2) void conv3x3_ring_kernel(const Ig
   };
   auto issue_w = [&](int g) {
     const int s = g - (g / S) * S;
-    const char* src = wblk + (size_t)s * WSLOT;
-    char* dst = lds + WOFF + (g % NS) * WSLOT + wave * WI * 1024;
+    const char* src = wblk + (size_t)s * SLOT;
+    char* dst = lds + WOFF + (g % NS) * SLOT + wave * WI * 1024;
 #pragma unroll
-    for (int j = 0; j < WI; ++j) glds16(src + j * 1024, dst + j * 1024);
+    for (int t = 0; t < TPS; ++t)
+#pragma unroll
+      for (int j = 0; j < WI; ++j) glds16(src + t * WSLOT + j * 1024, dst + t * WSLOT + j * 1024);
   };
 
   f32x4 acc[TC][TP];
@@ -1028,15 +1039,15 @@ __global__ __launch_bounds__(64 * WR * WPX, 2) void conv3x3_ring_kernel(const Ig
   }
   {
     const int young = total - 1 < NS - 2 ? total - 1 : NS - 2;   // W(1..NS-2) may stay in flight
-    ring_wait<WI, HI, NS - 2>(young, false);
+    ring_wait<TPS * WI, HI, NS - 2>(young, false);
   }
 
   // one step: A (weight) fragments stream through a 3-register ring two MFMA groups ahead;
   // sched_group_barrier pins the read/MFMA interleave (see step_sg above)
-  auto step = [&](int g, int hs, int tp) {
+  auto step = [&](int g, int hs, int tp, int tsub) {
     const int dy = tp / 3, dx = tp - (tp / 3) * 3;
     const char* Hs = lds + (hs & 1) * HALO_BYTES + (dy * 18 + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
-    const char* Ws = wrow + (g % NS) * WSLOT;
+    const char* Ws = wrow + (g % NS) * SLOT + tsub * WSLOT;
     frag_t bq[TP], ar[3];
 #pragma unroll
     for (int p = 0; p < TP; ++p) bq[p] = *reinterpret_cast<const frag_t*>(Hs + prow[p]);
@@ -1055,12 +1066,13 @@ __global__ __launch_bounds__(64 * WR * WPX, 2) void conv3x3_ring_kernel(const Ig
     }
   };
 
-  int c = 0, tap = 0, hseq = 0, item = 0;
+  int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
   for (int g = 0; g < total; ++g) {
     const bool hnext = tap == 0 && hseq + 1 < hseq_end;
     if (hnext) issue_halo(hseq + 1);
     if (g + NS - 1 < total) issue_w(g + NS - 1);
-    step(g, hseq, tap);
+#pragma unroll
+    for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
     // W(g+1) must have landed (and, at a chunk end, the next halo -- issued 8 steps earlier,
     // so older than W(g+1)).  Younger loads may stay in flight: W(g+2 .. g+NS-1) and a halo
     // issued within the last NS-2 steps (this chunk's tap < NS-2).
@@ -1068,11 +1080,11 @@ __global__ __launch_bounds__(64 * WR * WPX, 2) void conv3x3_ring_kernel(const Ig
       int young = total - 2 - g;
       young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
       const bool hyoung = wave < HLW && tap < NS - 2 && hseq + 1 < hseq_end;
-      if (ABL == 1 && tap != 8) ring_wait_nobar<WI, HI, NS - 2>(young, hyoung);   // ablation: barrier per chunk only
-      else ring_wait<WI, HI, NS - 2>(young, hyoung);
+      if (ABL == 1 && tap != SPC - 1) ring_wait_nobar<TPS * WI, HI, NS - 2>(young, hyoung);   // ablation: barrier per chunk only
+      else ring_wait<TPS * WI, HI, NS - 2>(young, hyoung);
     }
     bool tile_end = false;
-    if (++tap == 9) {
+    if (++tap == SPC) {
       tap = 0;
       ++hseq;
       if (++c == nch) {
@@ -1236,9 +1248,9 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0>
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0, int TPS = 1>
 static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
-  using G = RingGeom<T, WR, WPX, TCW, NS>;
+  using G = RingGeom<T, WR, WPX, TCW, NS, TPS>;
   if constexpr (EPI == EPI_HEAD && G::BR != 64) return hipErrorInvalidValue;
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
   if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
@@ -1247,7 +1259,7 @@ static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
   if (n_slots < 1) n_slots = 1;
   if (n_slots > n_mt) n_slots = n_mt;
   if constexpr (EPI != EPI_HEAD || G::BR == 64)
-    hipLaunchKernelGGL((conv3x3_ring_kernel<T, WR, WPX, TCW, NS, EPI, ABL>), dim3(a.n_ct * n_slots), dim3(64 * WR * WPX), 0,
+    hipLaunchKernelGGL((conv3x3_ring_kernel<T, WR, WPX, TCW, NS, EPI, ABL, TPS>), dim3(a.n_ct * n_slots), dim3(64 * WR * WPX), 0,
                        s, a);
   return hipGetLastError();
 }
@@ -1281,6 +1293,7 @@ static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
       case CFG_RING_R64: return launch_ring<T, 1, 4, 4, 4, EPI>(a, s);
       case CFG_RING_R128_NS3: return launch_ring<T, 1, 4, 8, 3, EPI>(a, s);
       case CFG_RING_R64_NS5: return launch_ring<T, 1, 4, 4, 5, EPI>(a, s);
+      case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 0, 3>(a, s);
       case CFG_FUSED_IN_W4:
       case CFG_FUSED_IN_W8:
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) {
