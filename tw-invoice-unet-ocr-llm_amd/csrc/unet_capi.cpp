@@ -257,14 +257,22 @@ int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::v
 }
 
 // ConvTranspose2d(k2,s2): natural GEMM row R = (a*2+b)*cout + o; packed[rho][c] = W[c][o][a][b]
+// ConvTranspose2d (Cin, Cout, 2, 2) as GEMM rows (a, b, o): packed[rho][c]; the ring kernel
+// (cfg_is_tring) takes them in step order per 128-row tile: [ct][c / BKE][BR][BKE].
 int packT(unet_handle* h, Layer& L, const float* W, const float* B) {
   const int R = 4 * L.cout;
   std::vector<uint8_t> buf((size_t)R * L.cin * dtype_size(h->dt));
+  const bool ring = cfg_is_tring(L.cfg);
+  const int BR = cfg_rows(L.cfg), BKE = 64 / (int)dtype_size(h->dt), S = L.cin / BKE;
+  if (ring && (R % BR || L.cin % BKE)) return fail(UNET_EINVAL, "ring ConvTranspose tiling does not divide the layer");
   for (int rho = 0; rho < R; ++rho) {
     const int nat = natural_of_packed(rho);
     const int ab = nat / L.cout, o = nat % L.cout;
-    for (int c = 0; c < L.cin; ++c)
-      put_elem(h->dt, buf, (size_t)rho * L.cin + c, W[(((size_t)c * L.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]);
+    for (int c = 0; c < L.cin; ++c) {
+      const size_t idx = ring ? (((size_t)(rho / BR) * S + c / BKE) * BR + rho % BR) * BKE + c % BKE
+                              : (size_t)rho * L.cin + c;
+      put_elem(h->dt, buf, idx, W[(((size_t)c * L.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]);
+    }
   }
   std::vector<float> bias(R);
   for (int r = 0; r < R; ++r) bias[r] = B[r % L.cout];
@@ -360,6 +368,8 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
       {1, 4, 8, 1, 2, 7}, {1, 4, 8, 1, 3, 7}, {1, 4, 4, 1, 3, 7}, {1, 8, 4, 1, 3, 7}};
   if (cfg >= CFG_COUNT) {
     std::snprintf(buf, sizeof buf, "ablation_%d<%s, %d>", cfg - CFG_COUNT, tname(t), epi);
+  } else if (cfg_is_tring(cfg)) {
+    std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, 3>", tname(t));
   } else if (cfg_is_ring(cfg)) {
     const int tc = cfg_rows(cfg) / 16;
     std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, 0, %d>", tname(t), tc, ring_ns(cfg), epi,
@@ -460,7 +470,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     } else {
       // 16-bit: the 64-byte-row ring kernel on the 128-row layers (A/B: profiles/tune_r1_ring.txt);
       // fp32 stays on the 128-byte halo kernel
-      L.cfg = (cfg->dtype != UNET_DTYPE_F32 && i >= 1 && i <= 14) ? (int)CFG_RING_R128_NS3 : kDefaultCfg[i];
+      L.cfg = cfg->dtype == UNET_DTYPE_F32 ? kDefaultCfg[i]
+              : (i >= 1 && i <= 14) ? (int)CFG_RING_R128_NS3 : (i == C1A || i == C1B) ? (int)CFG_RING_R64_T3 : kDefaultCfg[i];
     }
   }
   if (ps == "gather") h->L[C1B].cfg = CFG_R64_P128;
@@ -474,7 +485,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
       const size_t colon = item.find(':');
       if (colon != std::string::npos) {
         const int li = std::atoi(item.substr(0, colon).c_str()), c = std::atoi(item.substr(colon + 1).c_str());
-        if (li >= 0 && li < 17 && c >= 0 && c < cfg_limit()) h->L[li].cfg = c;
+        if (li >= 0 && li < 17 && c >= 0 && c < cfg_limit() && !cfg_is_tring(c)) h->L[li].cfg = c;
       }
       pos = end + 1;
     }
@@ -500,7 +511,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     h->U[i].cout = kUpCh[i][1];
     h->U[i].ctot = 4 * kUpCh[i][1];
     h->U[i].taps = 1;
-    h->U[i].cfg = ps == "gather" ? CFG_R128_P128 : kDefaultUpCfg[i];
+    h->U[i].cfg = ps == "gather" ? CFG_R128_P128 : (cfg->dtype == UNET_DTYPE_F32 ? kDefaultUpCfg[i] : (int)CFG_TRING_R128);
   }
   if (const char* ov = std::getenv("UNET_MI355X_UPCFG")) {   // "i:cfg,..." i = 0..3 (up4..up1)
     std::string o(ov);
@@ -515,7 +526,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
         if (li >= 0 && li < 4 && (c == CFG_R128_P128 || c == CFG_R64_P128 || c == CFG_HALO1_R64_W4 ||
                                   c == CFG_HALO1_R128T8_NS2 || c == CFG_HALO_R128_W8 || c == CFG_HALO1_R64_W8 ||
                                   c == CFG_HALO1_R128T8_NS3 || c == CFG_HALO_R128_W4 || c == CFG_HALO3_R64_W8 ||
-                                  c == CFG_HALO3_R64_W4 || c == CFG_SG_R128T8_NS2 || c == CFG_SG_R64_W4))
+                                  c == CFG_HALO3_R64_W4 || c == CFG_SG_R128T8_NS2 || c == CFG_SG_R64_W4 ||
+                                  c == CFG_TRING_R128))
           h->U[li].cfg = c;
       }
       pos = end + 1;

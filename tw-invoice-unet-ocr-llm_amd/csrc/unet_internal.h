@@ -89,7 +89,9 @@ enum Cfg : int {
   CFG_RING_R128 = 27, CFG_RING_R64 = 28, CFG_RING_R128_NS3 = 29, CFG_RING_R64_NS5 = 30,
   // 64-row ring stepping one kernel row (3 taps, 48 MFMAs per wave) per barrier, 3 slots of 3 taps
   CFG_RING_R64_T3 = 31,
-  CFG_COUNT = 32
+  // ConvTranspose only: persistent ring GEMM, A and B through one 3-slot LDS-DMA ring (64-byte K steps)
+  CFG_TRING_R128 = 32,
+  CFG_COUNT = 33
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);
@@ -98,6 +100,7 @@ bool cfg_is_halo(int cfg);
 bool cfg_is_ring(int cfg);   // 64-byte-row ring kernel: step-major packed weights
 int ring_ns(int cfg);       // ring kernel: weight-ring slots
 int ring_tps(int cfg);      // ring kernel: taps per step
+bool cfg_is_tring(int cfg); // ConvTranspose ring kernel: step-major packed weights
 int cfg_limit();   // number of valid Cfg values in this build
 
 hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s);

@@ -37,7 +37,7 @@ int cfg_rows(int cfg) {
   return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8 ||
           cfg == CFG_HALO1_R128_W4 || cfg == CFG_PHALO_R128_W8 || cfg == CFG_HALO1_R128T8_NS2 ||
           cfg == CFG_HALO1_R128T8_NS3 || cfg == CFG_SG_R128T8_NS2 || cfg == CFG_SG_R128T8_NS3 ||
-          cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3) ? 128 : 64;
+          cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3 || cfg == CFG_TRING_R128) ? 128 : 64;
 }
 bool cfg_single_chunk(int cfg) { (void)cfg; return false; }
 int cfg_pixels(int cfg) {
@@ -50,6 +50,7 @@ int ring_ns(int cfg) {
   return (cfg == CFG_RING_R128_NS3 || cfg == CFG_RING_R64_T3) ? 3 : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
 }
 int ring_tps(int cfg) { return cfg == CFG_RING_R64_T3 ? 3 : 1; }
+bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128; }
 int cfg_limit() {
 #ifdef UNET_ABLATION
   return CFG_COUNT + 15;
@@ -1110,6 +1111,149 @@ __global__ __launch_bounds__(64 * WR * WPX, 2) void conv3x3_ring_kernel(const Ig
 }
 
 // ---------------------------------------------------------------------------------
+// ConvTranspose2d(k2, s2) as a persistent ring GEMM (up4 .. up1)
+// ---------------------------------------------------------------------------------
+// GEMM rows = (a, b, cout) (4 * Cout, packed per 128-row tile in step order like the 3x3 ring),
+// K = Cin in 64-byte steps, columns = a 16x16 input-pixel tile; the pixel-shuffle store of the
+// shared epilogue writes output pixels (2y+a, 2x+b) into the concat buffer.  K is short (2..32
+// steps per tile at 64 B), so instead of the halo kernel's one-tile-per-block prologue both
+// operands stream through ONE NS-slot LDS-DMA ring that runs across tile boundaries of a
+// persistent walker: the next tile's first steps load during this tile's last MFMAs and its
+// scatter epilogue.  LDS per slot: A [BR][64 B] (chunk q of row r at q ^ ((r >> 1) & 3)) +
+// B [256 px][64 B] (pixel row py*16+px, chunk q at q ^ ((py & 1) << 1): conflict-free for all
+// ds_read_b128 lane groups and pixel groups, checked exhaustively).
+template <typename T, int TCW, int NS>
+__global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
+  constexpr int NW = 4, TC = TCW, TP = 4, BR = 16 * TC, BKE = 64 / (int)sizeof(T);
+  constexpr int WI = BR / (16 * NW);          // A DMA instructions per wave and step
+  constexpr int BI = 256 / (16 * NW);         // B DMA instructions per wave and step
+  constexpr int ASLOT = BR * 64, BSLOT = 256 * 64, SLOT = ASLOT + BSLOT;
+  constexpr int PARAM_OFF = NS * SLOT;
+  static_assert(NS == 3 && TC % 4 == 0, "ring depth / row tile");
+  __shared__ __attribute__((aligned(16))) char lds[PARAM_OFF + BR * 4];
+  float* bias_s = reinterpret_cast<float*>(lds + PARAM_OFF);
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int bid;
+  {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one walker
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
+    const int b = blockIdx.x, x = b & 7, k = b >> 3;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  }
+  const int ct = bid % a.n_ct;
+  const int slot = bid / a.n_ct;
+  const int n_slots = gridDim.x / a.n_ct;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  if (slot >= n_mt) return;
+  const int items = (n_mt - slot + n_slots - 1) / n_slots;
+  const int H = a.H, W = a.W;
+  const int S = a.Cin / BKE;
+  const int total = items * S;
+
+  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * ASLOT +
+                     (wave * WI * 16 + (lane >> 2)) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
+  const char* in = reinterpret_cast<const char*>(a.in);
+  const char* zero = reinterpret_cast<const char*>(a.zero);
+  auto tile_of = [&](int i, int& n, int& ty, int& tx) {
+    int mt = slot + i * n_slots;
+    tx = mt % a.tiles_x;
+    mt /= a.tiles_x;
+    ty = mt % a.tiles_y;
+    n = mt / a.tiles_y;
+  };
+  auto issue = [&](int g) {
+    const int i = g / S, c = g - (g / S) * S;
+    char* As = lds + (g % NS) * SLOT;
+#pragma unroll
+    for (int j = 0; j < WI; ++j) glds16(wblk + (size_t)c * ASLOT + j * 1024, As + (wave * WI + j) * 1024);
+    int n, ty, tx;
+    tile_of(i, n, ty, tx);
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int r = (wave * BI + j) * 16 + (lane >> 2), py = r >> 4, px = r & 15;
+      const int iy = ty * 16 + py, ix = tx * 16 + px;
+      const int chk = ((lane & 3) ^ ((py & 1) << 1)) << 4;
+      const bool ok = iy < H && ix < W;
+      const char* src = ok ? in + (((long long)(n * H + iy) * W + ix) * a.ldi + (long long)c * BKE) * (long long)sizeof(T) + chk
+                           : zero + chk;
+      glds16(src, As + ASLOT + (wave * BI + j) * 1024);
+    }
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int t = 0; t < TC; ++t)
+#pragma unroll
+    for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int col = lane & 15, q = lane >> 4;
+  int prow[TP];
+#pragma unroll
+  for (int p = 0; p < TP; ++p) {
+    int py, px;
+    pix_of((wave * TP + p) * 16 + col, py, px);
+    prow[p] = (py * 16 + px) * 64 + ((q ^ ((py & 1) << 1)) << 4);
+  }
+  const int wrow = col * 64 + ((q ^ ((col >> 1) & 3)) << 4);
+
+  issue(0);
+  if (total > 1) issue(1);
+  for (int i = tid; i < BR; i += 256) bias_s[i] = a.bias[ct * BR + i];
+  if (total > 1) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
+
+  int c = 0, item = 0;
+  for (int g = 0; g < total; ++g) {
+    if (g + 2 < total) issue(g + 2);
+    const char* As = lds + (g % NS) * SLOT + wrow;
+    const char* Bs = lds + (g % NS) * SLOT + ASLOT;
+    frag_t bq[TP], ar[3];
+#pragma unroll
+    for (int p = 0; p < TP; ++p) bq[p] = *reinterpret_cast<const frag_t*>(Bs + prow[p]);
+    ar[0] = *reinterpret_cast<const frag_t*>(As);
+    ar[1] = *reinterpret_cast<const frag_t*>(As + 16 * 64);
+    __builtin_amdgcn_sched_group_barrier(0x100, TP + 2, 0);
+#pragma unroll
+    for (int t = 0; t < TC; ++t) {
+      if (t + 2 < TC) ar[(t + 2) % 3] = *reinterpret_cast<const frag_t*>(As + (t + 2) * 16 * 64);
+      const frag_t af = ar[t % 3];
+#pragma unroll
+      for (int p = 0; p < TP; ++p)
+        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
+      if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+    }
+    // step g+1 must have landed; step g+2 (issued above) may stay in flight
+    if (g + 2 < total) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
+    if (++c == S) {
+      c = 0;
+      int n, ty, tx;
+      tile_of(item, n, ty, tx);
+#pragma unroll
+      for (int h = 0; h < TC / 4; ++h)
+        conv_epilogue<T, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
+                                            tx * 16, wave * TP, ct * BR + 64 * h, bias_s + 64 * h, nullptr, nullptr);
+#pragma unroll
+      for (int t = 0; t < TC; ++t)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ++item;
+    }
+  }
+}
+
+template <typename T, int TCW, int NS>
+static hipError_t launch_tring(const IgemmArgs& a, hipStream_t s) {
+  constexpr int BR = 16 * TCW, LDS = NS * (BR * 64 + 256 * 64) + BR * 4;
+  if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
+  if (a.Cin % (64 / (int)sizeof(T)) || a.Ctot % BR || a.n_ct != a.Ctot / BR) return hipErrorInvalidValue;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  int n_slots = (kNumCUs * ((160 * 1024) / LDS)) / a.n_ct;
+  if (n_slots < 1) n_slots = 1;
+  if (n_slots > n_mt) n_slots = n_mt;
+  hipLaunchKernelGGL((convT_ring_kernel<T, TCW, NS>), dim3(a.n_ct * n_slots), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
 // first conv: C in {1,3} input channels, fp32 NCHW in, 64 channels NHWC out.
 // K = 9*C is far too short for MFMA; it is a VALU direct conv, bound by HBM
 // (read 4*C B + write 64*sizeof(T) B per pixel).
@@ -1355,6 +1499,7 @@ static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipSt
       case CFG_HALO_R128_W4: return launch_halo<T, 1, 4, 8, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_HALO3_R64_W8: return launch_halo<T, 1, 8, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_HALO3_R64_W4: return launch_halo<T, 1, 4, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
+      case CFG_TRING_R128: return launch_tring<T, 8, 3>(a, s);
       default: return launch_cfg<T, 1, EPI_UPSCATTER>(cfg, a, s);
     }
   }
