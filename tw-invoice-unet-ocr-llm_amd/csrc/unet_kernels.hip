@@ -925,7 +925,7 @@ __device__ __forceinline__ void ring_wait(int nw, bool halo) {
 // between barriers and its ring slot holds TPS taps of weights (contiguous in the step-order
 // packing, so the pack is the same).
 template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0, int TPS = 1>
-__global__ __launch_bounds__(64 * WR * WPX, 2) void conv3x3_ring_kernel(const IgemmArgs a) {
+__global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_ring_kernel(const IgemmArgs a) {
   using G = RingGeom<T, WR, WPX, TCW, NS, TPS>;
   constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
   constexpr int HI = G::HI, WI = G::WI, HLW = G::HLW, HALO_BYTES = G::HALO_BYTES, WSLOT = G::WSLOT;
@@ -1399,7 +1399,8 @@ static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
   if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
-  int n_slots = (kNumCUs * G::BLOCKS_PER_CU) / a.n_ct;
+  constexpr int per_cu = G::NW >= 8 ? 1 : G::BLOCKS_PER_CU;   // 8-wave blocks: registers allow one per CU
+  int n_slots = (kNumCUs * per_cu) / a.n_ct;
   if (n_slots < 1) n_slots = 1;
   if (n_slots > n_mt) n_slots = n_mt;
   if constexpr (EPI != EPI_HEAD || G::BR == 64)
