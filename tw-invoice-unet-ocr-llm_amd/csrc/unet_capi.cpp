@@ -505,7 +505,6 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
                            : (ring ? CFG_RING_R128_NS3 : halo ? CFG_HALO1_R128T8_NS2 : CFG_R128_P128);
     if (i == C1B && cfg_rows(L.cfg) != 64) L.cfg = ring ? CFG_RING_R64 : halo ? CFG_HALO1_R64_W8 : CFG_R64_P128;
   }
-  build_labels(h);
   for (int i = 0; i < 4; ++i) {
     h->U[i].cin = kUpCh[i][0];
     h->U[i].cout = kUpCh[i][1];
@@ -533,6 +532,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
       pos = end + 1;
     }
   }
+  build_labels(h);   // after every layer's configuration (3x3 and ConvTranspose) is final
   DeviceGuard g(cfg->device);
   std::vector<uint8_t> z(256, 0);
   int rc = upload(h, &h->zero, z.data(), z.size());
