@@ -185,9 +185,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]   # per-step spread (diagnostic)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    ev[0].record()
+    for i in range(args.steps):
         step()
+        ev[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -197,6 +200,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = 1e3 * elapsed / args.steps
+    step_ms = [round(ev[i].elapsed_time(ev[i + 1]), 3) for i in range(args.steps)]
     value = world * B * args.steps / elapsed
 
     # ---- per-launch HIP-event timing (same stream) -> dominant kernel roofline
@@ -213,7 +217,7 @@ def main():
             k["gflop"] += launch_flops(entry, B, S, S, C) / 1e9
             k["algo_gb"] += launch_bytes(entry, B, S, S, C, esize) / 1e9
             k["layers"].append(entry[0])
-        dom_name, dom = max(((n, k) for n, k in kernels.items() if "first_conv" not in n),
+        dom_name, dom = max(((n, k) for n, k in kernels.items() if "first_conv" not in n and "x_to_px4" not in n),
                             key=lambda kv: kv[1]["ms"])
         achieved = dom["gflop"] / dom["ms"]   # TFLOP/s (GFLOP / ms)
         for k in kernels.values():
@@ -271,7 +275,7 @@ def main():
                                    f"threshold bit-packed masks" + (" + RCCL all-gather" if world > 1 else ""),
                        "global_batch": world * B, "per_gpu_batch": B, "image": S,
                        "parallelism": f"dp{world}"},
-            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "layer_ms": layer_ms,
+            "roofline": roofline, "cpu_baseline": cpu, "step_ms": step_ms, "kernels": kernels, "layer_ms": layer_ms,
         }
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

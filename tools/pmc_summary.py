@@ -69,7 +69,7 @@ def main():
             continue
         rows = load_pass(p)
         ours = [(did, v) for did, v in sorted(rows.items())
-                if any(s in v[0] for s in ("igemm", "first_conv", "halo", "ring_kernel"))]
+                if any(s in v[0] for s in ("igemm", "first_conv", "halo", "ring_kernel", "x_to_px4"))]
         last = ours[-len(launches):]
         for i, (did, (name, ctr)) in enumerate(last):
             per_launch[i].update(ctr)

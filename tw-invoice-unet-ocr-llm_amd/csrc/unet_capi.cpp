@@ -68,7 +68,7 @@ inline int natural_of_packed(int rho) {
   return g + (r >> 2) * 16 + t * 4 + (r & 3);
 }
 
-bool is_fused_in(int cfg) { return cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8; }
+bool is_fused_in(int cfg) { return cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8 || cfg == CFG_RING_FUSED_IN; }
 
 struct Layer {
   int cin = 0, cout = 0, ctot = 0, taps = 9, cfg = CFG_R128_P128;
@@ -83,7 +83,7 @@ struct ResampleStore {
 };
 
 struct Buffers {
-  size_t tA, cat1, cat2, cat3, cat4, p1, p2, p3, p4, bnb, tB, mbits, total;  // byte offsets
+  size_t tA, cat1, cat2, cat3, cat4, p1, p2, p3, p4, bnb, tB, mbits, xpx, total;  // byte offsets
 };
 
 }  // namespace
@@ -93,6 +93,8 @@ struct unet_handle {
   DType dt = DType::BF16;
   float* w0 = nullptr;  // first conv folded fp32 [64][C][3][3]
   void* w0p = nullptr;  // first conv packed [64][32] element type (16-bit MFMA path)
+  void* w0r = nullptr;  // the same, rows ordered for the ring kernel's fused first conv:
+                        // [cb][t][16][32], row (cb, t, r) = channel 32cb + 8(r>>2) + 4t + (r&3)
   float* b0 = nullptr;
   Layer L[17];          // d1b d2a d2b d3a d3b d4a d4b bna bnb c4a c4b c3a c3b c2a c2b c1a c1b
   Layer U[4];           // up4 up3 up2 up1
@@ -163,6 +165,7 @@ Buffers plan(DType dt, int N, int H, int W) {
   b.tB = take(P / 4 * 128);
   b.mbits = o;   // bit-packed masks for unet_forward_boxes without caller masks (<= kMaxClasses fields)
   o = align256(o + (size_t)kMaxClasses * P / 8);
+  b.xpx = take(P * 4);   // network input as T [N][H][W][4] for the ring kernel's fused first conv
   b.total = o;
   return b;
 }
@@ -372,8 +375,8 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
     std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, 3>", tname(t));
   } else if (cfg_is_ring(cfg)) {
     const int tc = cfg_rows(cfg) / 16;
-    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, 0, %d>", tname(t), tc, ring_ns(cfg), epi,
-                  ring_tps(cfg));
+    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %d>", tname(t), tc, ring_ns(cfg),
+                  epi, ring_abl(cfg), ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0);
   } else if (cfg_is_halo(cfg)) {
     const auto& c = halo[cfg - CFG_HALO_R128_W4];
     const int hsrc = (cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8) ? 1 : 0;
@@ -396,7 +399,13 @@ void build_labels(unet_handle* h) {
                                         101, C3A, C3B, 102, C2A, C2B, 103, C1A, C1B};
   for (int i = 0; i < UNET_NUM_LAUNCHES; ++i) {
     const int id = order[i];
-    if (id < 0) { h->labels[i] = is_fused_in(h->L[D1B].cfg) ? "fused_into_down1.3" : buf; continue; }
+    if (id < 0) {
+      if (h->L[D1B].cfg == CFG_RING_FUSED_IN)
+        h->labels[i] = std::string("x_to_px4_kernel<") + tname(h->dt) + ">";   // pre-cast; conv fused into down1.3
+      else
+        h->labels[i] = is_fused_in(h->L[D1B].cfg) ? "fused_into_down1.3" : buf;
+      continue;
+    }
     if (id >= 100) { h->labels[i] = layer_label(h->dt, h->U[id - 100].cfg, 1, EPI_UPSCATTER); continue; }
     const int epi = id == C1B ? EPI_HEAD : (id == D1B || id == D2B || id == D3B || id == D4B) ? EPI_POOL : EPI_STORE;
     h->labels[i] = layer_label(h->dt, h->L[id].cfg, 9, epi);
@@ -471,7 +480,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
       // 16-bit: the 64-byte-row ring kernel on the 128-row layers (A/B: profiles/tune_r1_ring.txt);
       // fp32 stays on the 128-byte halo kernel
       L.cfg = cfg->dtype == UNET_DTYPE_F32 ? kDefaultCfg[i]
-              : (i >= 1 && i <= 14) ? (int)CFG_RING_R128_NS3 : (i == C1A || i == C1B) ? (int)CFG_RING_R64_T3 : kDefaultCfg[i];
+              : (i >= 1 && i <= 14) ? (int)CFG_RING_R128_NS3 : (i == C1A || i == C1B) ? (int)CFG_RING_R64_T3
+              : (i == D1B) ? (int)CFG_RING_FUSED_IN : kDefaultCfg[i];
     }
   }
   if (ps == "gather") h->L[C1B].cfg = CFG_R64_P128;
@@ -492,14 +502,15 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   }
   for (int i = 0; i < 17; ++i) {   // keep every layer on a configuration it supports
     Layer& L = h->L[i];
-    const bool fused_in = L.cfg == CFG_FUSED_IN_W4 || L.cfg == CFG_FUSED_IN_W8;
+    const bool fused_in = is_fused_in(L.cfg);
     // fall back within the same kernel family (LDS-halo configurations all accumulate in the
     // same K order, so they agree bitwise; the gather kernels order K differently)
     // (the ring kernels share one K order among themselves, chunk32-major)
     const bool ring = cfg_is_ring(L.cfg);
     const bool halo = cfg_is_halo(L.cfg) && !ring;
     if (fused_in && (i != D1B || cfg->dtype == UNET_DTYPE_F32))
-      L.cfg = L.cout == 64 ? CFG_HALO1_R64_W8 : CFG_HALO1_R128T8_NS2;
+      L.cfg = L.cfg == CFG_RING_FUSED_IN ? (L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128_NS3)
+                                         : (L.cout == 64 ? CFG_HALO1_R64_W8 : CFG_HALO1_R128T8_NS2);
     if (cfg_rows(L.cfg) > L.cout || L.cfg == CFG_R128_P256 || (cfg_single_chunk(L.cfg) && L.cin != chunk))
       L.cfg = L.cout == 64 ? (ring ? CFG_RING_R64 : halo ? CFG_HALO1_R64_W8 : CFG_R64_P256)
                            : (ring ? CFG_RING_R128_NS3 : halo ? CFG_HALO1_R128T8_NS2 : CFG_R128_P128);
@@ -570,6 +581,7 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
     if (!rc) rc = upload(h, (void**)&h->b0, bf.data(), bf.size() * 4);
     if (rc) return rc;
     h->w0p = nullptr;
+    h->w0r = nullptr;
     if (h->dt != DType::F32) {   // MFMA operand: [rho][k], k = c*9 + ky*3 + kx < 9C, zero pad to 32
       std::vector<uint8_t> pk((size_t)64 * 32 * 2, 0);
       for (int rho = 0; rho < 64; ++rho) {
@@ -577,6 +589,15 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
         for (int k = 0; k < 9 * C; ++k) put_elem(h->dt, pk, (size_t)rho * 32 + k, w[(size_t)o * 9 * C + k]);
       }
       rc = upload(h, &h->w0p, pk.data(), pk.size());
+      if (rc) return rc;
+      std::vector<uint8_t> pr((size_t)64 * 32 * 2, 0);
+      for (int cb = 0; cb < 2; ++cb)
+        for (int t = 0; t < 2; ++t)
+          for (int r = 0; r < 16; ++r) {
+            const int o = 32 * cb + 8 * (r >> 2) + 4 * t + (r & 3);
+            for (int k = 0; k < 9 * C; ++k) put_elem(h->dt, pr, ((size_t)(cb * 2 + t) * 16 + r) * 32 + k, w[(size_t)o * 9 * C + k]);
+          }
+      rc = upload(h, &h->w0r, pr.data(), pr.size());
       if (rc) return rc;
     }
   }
@@ -637,7 +658,7 @@ namespace {
 int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, int H, int W, int ldi,
               void* out, int ldo, int out_off, void* out2, int ldo2, hipStream_t s,
               float* logits = nullptr, void* masks = nullptr, int mask_kind = MASK_NONE,
-              const float* x0 = nullptr) {
+              const void* x0 = nullptr) {
   IgemmArgs a{};
   a.in = in;
   a.wgt = L.w;
@@ -657,7 +678,7 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.mask_kind = mask_kind;
   if (is_fused_in(L.cfg)) {
     a.x0 = x0;
-    a.w0p = h->w0p;
+    a.w0p = L.cfg == CFG_RING_FUSED_IN ? h->w0r : h->w0p;
     a.b0 = h->b0;
     a.c0 = h->cfg.n_channels;
   }
@@ -741,7 +762,12 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   auto mark = [&]() { if (ev) (void)hipEventRecord(ev[li], s); ++li; };
   mark();
   const bool fused_in = is_fused_in(h->L[D1B].cfg);   // down1.0 computed inside down1.3
-  if (!fused_in) {
+  const void* x0 = x;
+  if (h->L[D1B].cfg == CFG_RING_FUSED_IN) {   // the ring's fused first conv reads T [N][H][W][4]
+    hipError_t e = launch_x_to_px4(h->dt, static_cast<const float*>(x), N, h->cfg.n_channels, H, W, buf(B.xpx), s);
+    if (e != hipSuccess) return fail(UNET_EHIP, std::string("input pre-cast launch: ") + hipGetErrorString(e));
+    x0 = buf(B.xpx);
+  } else if (!fused_in) {
     hipError_t e = launch_first_conv(h->dt, f, s);
     if (e != hipSuccess) return fail(UNET_EHIP, std::string("first conv launch: ") + hipGetErrorString(e));
   }
@@ -750,7 +776,7 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   // encoder: conv b of each level writes the skip into the upper half of the concat
   // buffer (torch.cat([up, skip]) puts skip second, unet_model.py:71) and the pooled map.
   RUN(h, h->L[D1B], EPI_POOL, buf(B.tA), N, H, W, 64, buf(B.cat1), 128, 64, buf(B.p1), 64, s,
-      nullptr, nullptr, MASK_NONE, static_cast<const float*>(x));
+      nullptr, nullptr, MASK_NONE, x0);
   RUN(h, h->L[D2A], EPI_STORE, buf(B.p1), N, H2, W2, 64, buf(B.tA), 128, 0, nullptr, 0, s);
   RUN(h, h->L[D2B], EPI_POOL, buf(B.tA), N, H2, W2, 128, buf(B.cat2), 256, 128, buf(B.p2), 128, s);
   RUN(h, h->L[D3A], EPI_STORE, buf(B.p2), N, H4, W4, 128, buf(B.tA), 256, 0, nullptr, 0, s);

@@ -47,7 +47,8 @@ struct IgemmArgs {
   float thr_logit[kMaxClasses];   // logit cut per class: sigmoid(x) > thr  <=>  x > thr_logit
   int tiles_x, tiles_y, n_ct, n_blocks;
   // fused first conv (halo computed from the raw input instead of loaded): down1.0 + down1.3
-  const float* x0;     // NCHW fp32 network input [N][c0][H][W]
+  const void* x0;      // network input: NCHW fp32 [N][c0][H][W] (halo kernel), or T [N][H][W][4]
+                       // (CFG_RING_FUSED_IN, see launch_x_to_px4)
   const void* w0p;     // first conv packed [64][32] element type (rows permuted)
   const float* b0;     // first conv folded bias [64]
   int c0;              // network input channels (1 or 3)
@@ -91,7 +92,11 @@ enum Cfg : int {
   CFG_RING_R64_T3 = 31,
   // ConvTranspose only: persistent ring GEMM, A and B through one 3-slot LDS-DMA ring (64-byte K steps)
   CFG_TRING_R128 = 32,
-  CFG_COUNT = 33
+  // down1.0 fused into down1.3 on the 3-taps-per-step ring (halo chunks computed from the input)
+  CFG_RING_FUSED_IN = 33,
+  // s_setprio(1) around each step's MFMA cluster (cdna guide T5) on the R128 / R64-T3 rings
+  CFG_RING_R128_PRIO = 34, CFG_RING_R64_T3_PRIO = 35,
+  CFG_COUNT = 36
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);
@@ -100,11 +105,14 @@ bool cfg_is_halo(int cfg);
 bool cfg_is_ring(int cfg);   // 64-byte-row ring kernel: step-major packed weights
 int ring_ns(int cfg);       // ring kernel: weight-ring slots
 int ring_tps(int cfg);      // ring kernel: taps per step
+int ring_abl(int cfg);      // ring kernel: variant flag (2 = s_setprio around the MFMA clusters)
 bool cfg_is_tring(int cfg); // ConvTranspose ring kernel: step-major packed weights
 int cfg_limit();   // number of valid Cfg values in this build
 
 hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s);
 hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s);
+// fp32 NCHW input -> T [N][H][W][4] (input of the fused first conv of CFG_RING_FUSED_IN)
+hipError_t launch_x_to_px4(DType t, const float* x, int N, int C, int H, int W, void* out, hipStream_t s);
 // NHWC (pixel stride ld, channel offset choff, C channels) element type t -> NCHW fp32
 hipError_t launch_nhwc_to_nchw_f32(DType t, const void* src, int N, int H, int W, int C, int ld,
                                    int choff, float* dst, hipStream_t s);

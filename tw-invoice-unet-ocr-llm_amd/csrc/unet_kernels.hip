@@ -37,7 +37,8 @@ int cfg_rows(int cfg) {
   return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8 ||
           cfg == CFG_HALO1_R128_W4 || cfg == CFG_PHALO_R128_W8 || cfg == CFG_HALO1_R128T8_NS2 ||
           cfg == CFG_HALO1_R128T8_NS3 || cfg == CFG_SG_R128T8_NS2 || cfg == CFG_SG_R128T8_NS3 ||
-          cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3 || cfg == CFG_TRING_R128) ? 128 : 64;
+          cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3 || cfg == CFG_TRING_R128 || cfg == CFG_RING_R128_PRIO) ? 128
+                                                                                                     : 64;
 }
 bool cfg_single_chunk(int cfg) { (void)cfg; return false; }
 int cfg_pixels(int cfg) {
@@ -45,11 +46,18 @@ int cfg_pixels(int cfg) {
           cfg == CFG_T8_HALO_R64_W2) ? 128 : 256;
 }
 bool cfg_is_halo(int cfg) { return cfg >= CFG_HALO_R128_W4; }
-bool cfg_is_ring(int cfg) { return cfg >= CFG_RING_R128 && cfg <= CFG_RING_R64_T3; }
-int ring_ns(int cfg) {
-  return (cfg == CFG_RING_R128_NS3 || cfg == CFG_RING_R64_T3) ? 3 : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
+bool cfg_is_ring(int cfg) {
+  return (cfg >= CFG_RING_R128 && cfg <= CFG_RING_R64_T3) || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING_R128_PRIO ||
+         cfg == CFG_RING_R64_T3_PRIO;
 }
-int ring_tps(int cfg) { return cfg == CFG_RING_R64_T3 ? 3 : 1; }
+int ring_ns(int cfg) {
+  return (cfg == CFG_RING_R128_NS3 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING_R128_PRIO ||
+          cfg == CFG_RING_R64_T3_PRIO) ? 3 : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
+}
+int ring_tps(int cfg) {
+  return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING_R64_T3_PRIO) ? 3 : 1;
+}
+int ring_abl(int cfg) { return (cfg == CFG_RING_R128_PRIO || cfg == CFG_RING_R64_T3_PRIO) ? 2 : 0; }
 bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128; }
 int cfg_limit() {
 #ifdef UNET_ABLATION
@@ -614,7 +622,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
       const int c = i / (XSW * XSH), r = i - c * (XSW * XSH), yy = r / XSW, xx = r - (r / XSW) * XSW;
       const int iy = ty0 * TH + yy - 2, ix = tx0 * 16 + xx - 2;
       const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      xs[i] = ok ? a.x0[(((long long)n0 * C0 + c) * H + iy) * W + ix] : 0.f;
+      xs[i] = ok ? static_cast<const float*>(a.x0)[(((long long)n0 * C0 + c) * H + iy) * W + ix] : 0.f;
     }
     frag_t wf[4];
 #pragma unroll
@@ -880,7 +888,7 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
 // overlaps the loads of the next.
 constexpr int kRingPix = 18 * 18;
 
-template <typename T, int WR, int WPX, int TCW, int NS, int TPS = 1>
+template <typename T, int WR, int WPX, int TCW, int NS, int TPS = 1, int HS = 0>
 struct RingGeom {
   static constexpr int NW = WR * WPX;
   static constexpr int TC = TCW;
@@ -890,13 +898,16 @@ struct RingGeom {
   static constexpr int RPI = 16;                    // 64-byte rows per LDS-DMA instruction
   static constexpr int HLW = NW >= 7 ? 7 : (NW >= 3 ? 3 : NW);   // halo loader waves (21 instr.)
   static constexpr int HI = (kRingPix + RPI * HLW - 1) / (RPI * HLW);
-  static constexpr int HALO_BYTES = HI * HLW * RPI * 64;
+  // HS = 1: the halo is computed (fused first conv), not DMA'd: exactly 18x18 rows
+  static constexpr int HALO_BYTES = HS ? kRingPix * 64 : HI * HLW * RPI * 64;
   static constexpr int WI = BR / (RPI * NW);
   static constexpr int WSLOT = BR * 64;              // one tap's weights
   static constexpr int SLOT = TPS * WSLOT;           // one ring slot = one step = TPS taps
   static constexpr int WOFF = 2 * HALO_BYTES;
   static constexpr int PARAM_OFF = WOFF + NS * SLOT;
-  static constexpr int LDS_BYTES = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
+  static constexpr int XS_OFF = PARAM_OFF + (HS ? BR : BR + kMaxClasses * 64 + kMaxClasses) * 4;
+  static constexpr int XS_BYTES = HS ? 20 * 20 * 4 * (int)sizeof(T) : 0;   // 20x20 input window, 4 ch
+  static constexpr int LDS_BYTES = XS_OFF + XS_BYTES;
   static constexpr int BLOCKS_PER_CU = (160 * 1024) / LDS_BYTES;
 };
 
@@ -924,9 +935,14 @@ __device__ __forceinline__ void ring_wait(int nw, bool halo) {
 // TPS = taps per step (1, or 3 = one kernel row): a step then runs TPS x TC x TP MFMAs per wave
 // between barriers and its ring slot holds TPS taps of weights (contiguous in the step-order
 // packing, so the pack is the same).
-template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0, int TPS = 1>
+// HS = 1 (down1.3 only): down1.0 is fused in -- every 32-channel halo chunk is COMPUTED from a
+// 20x20 window of the network input (pre-cast to T, 4 channels per pixel, x_to_px4_kernel) on
+// MFMA (K = 9*C <= 27 padded to 32) and written to the halo buffer with ds_write, one chunk
+// ahead like the DMA halo; the window of the next tile is LDS-DMA'd (16-byte pieces, 2 pixels
+// per lane) into a single buffer after the current window's last use.
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0, int TPS = 1, int HS = 0>
 __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_ring_kernel(const IgemmArgs a) {
-  using G = RingGeom<T, WR, WPX, TCW, NS, TPS>;
+  using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS>;
   constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
   constexpr int HI = G::HI, WI = G::WI, HLW = G::HLW, HALO_BYTES = G::HALO_BYTES, WSLOT = G::WSLOT;
   constexpr int WOFF = G::WOFF, SLOT = G::SLOT;
@@ -936,6 +952,8 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
   static_assert(WI >= 1 && BR % (G::RPI * NW) == 0, "weight tile split");
   static_assert(TP >= 1 && 16 % WPX == 0, "pixel groups per wave");
   static_assert(EPI != EPI_HEAD || BR == 64, "fused head needs the 64 channels in one block");
+  static_assert(HS == 0 || (sizeof(T) == 2 && BR == 64 && NW == 4 && EPI != EPI_HEAD), "fused first conv: 16-bit, 64 rows");
+  static_assert(WR * WPX >= 8 || G::LDS_BYTES <= 160 * 1024 / 2, "two blocks per CU");
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
   float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
   float* headw_s = bias_s + BR;
@@ -1028,8 +1046,88 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
   const int wpos = (q ^ ((col >> 1) & 3)) << 4;
   const char* wrow = lds + WOFF + (wr * 16 * TC + col) * 64 + wpos;
 
+  // ---- HS: fused first conv (down1.0) -> halo chunks ----
+  // window DMA of tile i: lane L < 200 of the block's 4 pieces copies input pixels
+  // (2*(L%10), 2*(L%10)+1) of window row L/10 (8 B each) -> xs[(yy*20 + xx)*4 + c]
+  auto issue_xs = [&](int i) {
+    if constexpr (HS != 0) {
+      int n, ty, tx;
+      tile_of(i, n, ty, tx);
+      const int L = wave * 64 + lane;
+      if (L < 200) {
+        const int yy = L / 10, seg = L - (L / 10) * 10;
+        const int iy = ty * 16 + yy - 2, ix = tx * 16 + 2 * seg - 2;
+        const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        const char* src = ok ? reinterpret_cast<const char*>(a.x0) + ((long long)(n * H + iy) * W + ix) * 4 * sizeof(T)
+                             : zero;
+        glds16(src, lds + G::XS_OFF + wave * 1024);
+      }
+    }
+  };
+  // halo chunk cb (channels 32cb .. 32cb+31 of down1.0's output) of tile i -> halo buffer hb
+  frag_t w0f[2][2];
+  float b0v[2][8];
+  int xoff[8];
+  if constexpr (HS != 0) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        w0f[cb][t] = *reinterpret_cast<const frag_t*>(reinterpret_cast<const char*>(a.w0p) +
+                                                      (((cb * 2 + t) * 16 + (lane & 15)) * 32 + 8 * (lane >> 4)) * sizeof(T));
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b0v[cb][j] = a.b0[32 * cb + 8 * (lane >> 4) + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {   // k = 8q + j -> (channel, ky, kx) offset in the window
+      const int k = 8 * (lane >> 4) + j, c = k / 9, r = k - (k / 9) * 9;
+      xoff[j] = k < 9 * a.c0 ? ((r / 3) * 20 + (r - (r / 3) * 3)) * 4 + c : -1;
+    }
+  }
+  auto compute_halo = [&](int i, int cb, int hb) {
+    if constexpr (HS != 0) {
+      int n, ty, tx;
+      tile_of(i, n, ty, tx);
+      const T* xs = reinterpret_cast<const T*>(lds + G::XS_OFF);
+      char* dst = lds + hb * HALO_BYTES;
+      const int qq = lane >> 4;
+      for (int grp = wave; grp * 16 < kRingPix; grp += NW) {
+        const int p = grp * 16 + (lane & 15);
+        const bool real = p < kRingPix;
+        const int hy = real ? p / 18 : 0, hx = real ? p - (p / 18) * 18 : 0;
+        typedef T t8 __attribute__((ext_vector_type(8)));
+        t8 hv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hv[j] = xoff[j] >= 0 ? xs[(hy * 20 + hx) * 4 + xoff[j]] : (T)0.f;
+        const uint4 bfr = __builtin_bit_cast(uint4, hv);
+        f32x4 acc0[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+          mfma_frag<T>(acc0[t], __builtin_bit_cast(uint4, w0f[cb][t]), bfr);
+        }
+        // lane holds channels 32cb + 8q + 4t + e: 8 consecutive channels = one 16-byte piece
+        const int iy = ty * 16 + hy - 1, ix = tx * 16 + hx - 1;
+        const bool inimg = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        t8 o;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[4 * t + e] = (T)(inimg ? fmaxf(acc0[t][e] + b0v[cb][4 * t + e], 0.f) : 0.f);
+        if (real) *reinterpret_cast<uint4*>(dst + p * 64 + ((qq ^ (hx & 3)) << 4)) = __builtin_bit_cast(uint4, o);
+      }
+    }
+  };
+
   // prologue: halo of chunk 0 and weights of steps 0 .. NS-2
-  issue_halo(0);
+  if constexpr (HS != 0) {
+    issue_xs(0);
+    wait_vm_barrier<0>();
+    compute_halo(0, 0, 0);
+  } else {
+    issue_halo(0);
+  }
 #pragma unroll
   for (int k = 0; k < NS - 1; ++k)
     if (k < total) issue_w(k);
@@ -1055,6 +1153,7 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
     ar[0] = *reinterpret_cast<const frag_t*>(Ws);
     if (TC > 1) ar[1] = *reinterpret_cast<const frag_t*>(Ws + 16 * 64);
     __builtin_amdgcn_sched_group_barrier(0x100, TP + (TC > 1 ? 2 : 1), 0);
+    if constexpr (ABL == 2) __builtin_amdgcn_s_setprio(1);   // variant: raised priority over the MFMA cluster
 #pragma unroll
     for (int t = 0; t < TC; ++t) {
       if (t + 2 < TC) ar[(t + 2) % 3] = *reinterpret_cast<const frag_t*>(Ws + (t + 2) * 16 * 64);
@@ -1065,22 +1164,35 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
     }
+    if constexpr (ABL == 2) __builtin_amdgcn_s_setprio(0);
   };
 
   int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
   for (int g = 0; g < total; ++g) {
     const bool hnext = tap == 0 && hseq + 1 < hseq_end;
-    if (hnext) issue_halo(hseq + 1);
+    if constexpr (HS == 0) {
+      if (hnext) issue_halo(hseq + 1);
+    }
     if (g + NS - 1 < total) issue_w(g + NS - 1);
+    if constexpr (HS != 0) {
+      // the next tile's window, once this tile's last halo chunk has been computed from it (at
+      // chunk 0, step 0; the barrier after that step retired every read of xs).  Issued after
+      // this step's weights, so the wait at the end of the NEXT step (for those weights) is the
+      // one that retires it: two steps of latency before chunk 1 computes the next tile's halo.
+      if (c == 0 && tap == 1 && item + 1 < items) issue_xs(item + 1);
+    }
 #pragma unroll
     for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
+    if constexpr (HS != 0) {   // next chunk's halo into the other buffer (last read one step ago)
+      if (hnext) compute_halo(c + 1 < nch ? item : item + 1, c + 1 < nch ? c + 1 : 0, (hseq + 1) & 1);
+    }
     // W(g+1) must have landed (and, at a chunk end, the next halo -- issued 8 steps earlier,
     // so older than W(g+1)).  Younger loads may stay in flight: W(g+2 .. g+NS-1) and a halo
     // issued within the last NS-2 steps (this chunk's tap < NS-2).
     {
       int young = total - 2 - g;
       young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
-      const bool hyoung = wave < HLW && tap < NS - 2 && hseq + 1 < hseq_end;
+      const bool hyoung = HS == 0 && wave < HLW && tap < NS - 2 && hseq + 1 < hseq_end;
       if (ABL == 1 && tap != SPC - 1) ring_wait_nobar<TPS * WI, HI, NS - 2>(young, hyoung);   // ablation: barrier per chunk only
       else ring_wait<TPS * WI, HI, NS - 2>(young, hyoung);
     }
@@ -1392,9 +1504,12 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0, int TPS = 1>
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0, int TPS = 1, int HS = 0>
 static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
-  using G = RingGeom<T, WR, WPX, TCW, NS, TPS>;
+  using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS>;
+  if constexpr (HS != 0) {
+    if (a.Cin != 2 * G::BKE || a.c0 < 1 || a.c0 > 3 || !a.x0 || !a.w0p || !a.b0) return hipErrorInvalidValue;
+  }
   if constexpr (EPI == EPI_HEAD && G::BR != 64) return hipErrorInvalidValue;
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
   if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
@@ -1404,7 +1519,7 @@ static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
   if (n_slots < 1) n_slots = 1;
   if (n_slots > n_mt) n_slots = n_mt;
   if constexpr (EPI != EPI_HEAD || G::BR == 64)
-    hipLaunchKernelGGL((conv3x3_ring_kernel<T, WR, WPX, TCW, NS, EPI, ABL, TPS>), dim3(a.n_ct * n_slots), dim3(64 * WR * WPX), 0,
+    hipLaunchKernelGGL((conv3x3_ring_kernel<T, WR, WPX, TCW, NS, EPI, ABL, TPS, HS>), dim3(a.n_ct * n_slots), dim3(64 * WR * WPX), 0,
                        s, a);
   return hipGetLastError();
 }
@@ -1439,6 +1554,11 @@ static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
       case CFG_RING_R128_NS3: return launch_ring<T, 1, 4, 8, 3, EPI>(a, s);
       case CFG_RING_R64_NS5: return launch_ring<T, 1, 4, 4, 5, EPI>(a, s);
       case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 0, 3>(a, s);
+      case CFG_RING_R128_PRIO: return launch_ring<T, 1, 4, 8, 3, EPI, 2>(a, s);
+      case CFG_RING_R64_T3_PRIO: return launch_ring<T, 1, 4, 4, 3, EPI, 2, 3>(a, s);
+      case CFG_RING_FUSED_IN:
+        if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 0, 3, 1>(a, s);
+        return hipErrorInvalidValue;
       case CFG_FUSED_IN_W4:
       case CFG_FUSED_IN_W8:
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) {
@@ -1615,6 +1735,35 @@ hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, in
                              hipStream_t s) {
   if (W % 16 || W > kMaxBoxW || (kind != MASK_BITS && kind != MASK_U8)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mask_boxes_kernel, dim3((unsigned)(N * ncls)), dim3(256), 0, s, masks, kind, H, W, boxes);
+  return hipGetLastError();
+}
+
+// Network input pre-cast for the fused first conv of the ring kernel (HS = 1): fp32 NCHW
+// [N][C][H][W] -> element type T, 4 channels per pixel [N][H][W][4] (zero-padded), so a 20-pixel
+// window row is 160 contiguous bytes (10 LDS-DMA pieces).  The values are the (T) casts the
+// first conv's MFMA operand needs anyway.
+template <typename T>
+__global__ __launch_bounds__(256) void x_to_px4_kernel(const float* __restrict__ x, int N, int C, int H, int W,
+                                                      T* __restrict__ out) {
+  const long long P = (long long)N * H * W;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < P; i += (long long)gridDim.x * 256) {
+    const long long n = i / ((long long)H * W), hw = i - n * H * W;
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 v;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = (T)(c < C ? x[(n * C + c) * H * W + hw] : 0.f);
+    reinterpret_cast<t4*>(out)[i] = v;
+  }
+}
+
+hipError_t launch_x_to_px4(DType t, const float* x, int N, int C, int H, int W, void* out, hipStream_t s) {
+  const dim3 grid(4096), block(256);
+  if (t == DType::BF16)
+    hipLaunchKernelGGL(x_to_px4_kernel<__bf16>, grid, block, 0, s, x, N, C, H, W, static_cast<__bf16*>(out));
+  else if (t == DType::F16)
+    hipLaunchKernelGGL(x_to_px4_kernel<_Float16>, grid, block, 0, s, x, N, C, H, W, static_cast<_Float16*>(out));
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
