@@ -191,7 +191,7 @@ def test_weight_update_repacks():
     m.close()
 
 
-@pytest.mark.parametrize("cfg", list(range(36)))
+@pytest.mark.parametrize("cfg", list(range(34)))
 def test_every_kernel_config(cfg, monkeypatch):
     """Each implicit-GEMM configuration (csrc/unet_internal.h Cfg) forced on every 3x3 layer
     it supports, checked against the reference golden (fp32 and bf16)."""
@@ -257,7 +257,7 @@ def test_forward_deterministic_and_config_invariant(dtype, monkeypatch):
     forwards are bitwise identical, and within each kernel family every configuration --
     forced on all 3x3 layers, or on all ConvTranspose layers -- gives bitwise the same
     activations: the 128-byte LDS-halo configurations 4..26 (K order chunk64-major /
-    tap-minor) agree with each other, the 64-byte ring configurations 27..31, 33..35 (chunk32-major; 33 = down1.0 fused)
+    tap-minor) agree with each other, the 64-byte ring configurations 27..31 and 33 (chunk32-major; 33 = down1.0 fused)
     agree with each other, and the ConvTranspose configurations agree with the defaults.  A
     missed wait in a DMA ring shows up here as a run-to-run or config-to-config difference."""
     x = torch.from_numpy(syn.invoice_pages(3, 2, 512, 512, 3)).to(DEV)
@@ -268,7 +268,7 @@ def test_forward_deterministic_and_config_invariant(dtype, monkeypatch):
         assert _first_diff(_forward_state(m, x), base) == [], f"run {r + 1} differs"
     m.close()
     bad = []
-    for family in (list(range(4, 27)), list(range(27, 32)) + [33, 34, 35]):
+    for family in (list(range(4, 27)), list(range(27, 32)) + [33]):
         fbase = _forced(family[0], None, sd, x, dtype, monkeypatch)
         for cfg in family[1:]:
             d = _first_diff(_forced(cfg, None, sd, x, dtype, monkeypatch), fbase)

@@ -375,8 +375,8 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
     std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, 3>", tname(t));
   } else if (cfg_is_ring(cfg)) {
     const int tc = cfg_rows(cfg) / 16;
-    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %d>", tname(t), tc, ring_ns(cfg),
-                  epi, ring_abl(cfg), ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0);
+    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, 0, %d, %d>", tname(t), tc, ring_ns(cfg),
+                  epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0);
   } else if (cfg_is_halo(cfg)) {
     const auto& c = halo[cfg - CFG_HALO_R128_W4];
     const int hsrc = (cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8) ? 1 : 0;

@@ -94,9 +94,7 @@ enum Cfg : int {
   CFG_TRING_R128 = 32,
   // down1.0 fused into down1.3 on the 3-taps-per-step ring (halo chunks computed from the input)
   CFG_RING_FUSED_IN = 33,
-  // s_setprio(1) around each step's MFMA cluster (cdna guide T5) on the R128 / R64-T3 rings
-  CFG_RING_R128_PRIO = 34, CFG_RING_R64_T3_PRIO = 35,
-  CFG_COUNT = 36
+  CFG_COUNT = 34
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);
@@ -105,7 +103,6 @@ bool cfg_is_halo(int cfg);
 bool cfg_is_ring(int cfg);   // 64-byte-row ring kernel: step-major packed weights
 int ring_ns(int cfg);       // ring kernel: weight-ring slots
 int ring_tps(int cfg);      // ring kernel: taps per step
-int ring_abl(int cfg);      // ring kernel: variant flag (2 = s_setprio around the MFMA clusters)
 bool cfg_is_tring(int cfg); // ConvTranspose ring kernel: step-major packed weights
 int cfg_limit();   // number of valid Cfg values in this build
 

@@ -37,8 +37,7 @@ int cfg_rows(int cfg) {
   return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8 ||
           cfg == CFG_HALO1_R128_W4 || cfg == CFG_PHALO_R128_W8 || cfg == CFG_HALO1_R128T8_NS2 ||
           cfg == CFG_HALO1_R128T8_NS3 || cfg == CFG_SG_R128T8_NS2 || cfg == CFG_SG_R128T8_NS3 ||
-          cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3 || cfg == CFG_TRING_R128 || cfg == CFG_RING_R128_PRIO) ? 128
-                                                                                                     : 64;
+          cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3 || cfg == CFG_TRING_R128) ? 128 : 64;
 }
 bool cfg_single_chunk(int cfg) { (void)cfg; return false; }
 int cfg_pixels(int cfg) {
@@ -46,18 +45,12 @@ int cfg_pixels(int cfg) {
           cfg == CFG_T8_HALO_R64_W2) ? 128 : 256;
 }
 bool cfg_is_halo(int cfg) { return cfg >= CFG_HALO_R128_W4; }
-bool cfg_is_ring(int cfg) {
-  return (cfg >= CFG_RING_R128 && cfg <= CFG_RING_R64_T3) || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING_R128_PRIO ||
-         cfg == CFG_RING_R64_T3_PRIO;
-}
+bool cfg_is_ring(int cfg) { return (cfg >= CFG_RING_R128 && cfg <= CFG_RING_R64_T3) || cfg == CFG_RING_FUSED_IN; }
 int ring_ns(int cfg) {
-  return (cfg == CFG_RING_R128_NS3 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING_R128_PRIO ||
-          cfg == CFG_RING_R64_T3_PRIO) ? 3 : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
+  return (cfg == CFG_RING_R128_NS3 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN) ? 3
+                                                                                         : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
 }
-int ring_tps(int cfg) {
-  return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING_R64_T3_PRIO) ? 3 : 1;
-}
-int ring_abl(int cfg) { return (cfg == CFG_RING_R128_PRIO || cfg == CFG_RING_R64_T3_PRIO) ? 2 : 0; }
+int ring_tps(int cfg) { return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN) ? 3 : 1; }
 bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128; }
 int cfg_limit() {
 #ifdef UNET_ABLATION
@@ -1153,7 +1146,6 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
     ar[0] = *reinterpret_cast<const frag_t*>(Ws);
     if (TC > 1) ar[1] = *reinterpret_cast<const frag_t*>(Ws + 16 * 64);
     __builtin_amdgcn_sched_group_barrier(0x100, TP + (TC > 1 ? 2 : 1), 0);
-    if constexpr (ABL == 2) __builtin_amdgcn_s_setprio(1);   // variant: raised priority over the MFMA cluster
 #pragma unroll
     for (int t = 0; t < TC; ++t) {
       if (t + 2 < TC) ar[(t + 2) % 3] = *reinterpret_cast<const frag_t*>(Ws + (t + 2) * 16 * 64);
@@ -1164,7 +1156,6 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
     }
-    if constexpr (ABL == 2) __builtin_amdgcn_s_setprio(0);
   };
 
   int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
@@ -1554,8 +1545,6 @@ static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
       case CFG_RING_R128_NS3: return launch_ring<T, 1, 4, 8, 3, EPI>(a, s);
       case CFG_RING_R64_NS5: return launch_ring<T, 1, 4, 4, 5, EPI>(a, s);
       case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 0, 3>(a, s);
-      case CFG_RING_R128_PRIO: return launch_ring<T, 1, 4, 8, 3, EPI, 2>(a, s);
-      case CFG_RING_R64_T3_PRIO: return launch_ring<T, 1, 4, 4, 3, EPI, 2, 3>(a, s);
       case CFG_RING_FUSED_IN:
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 0, 3, 1>(a, s);
         return hipErrorInvalidValue;
