@@ -42,7 +42,14 @@ def main():
             p[k] = v.contiguous(memory_format=torch.channels_last)
     x = torch.from_numpy(syn.invoice_pages(1000, a.batch, a.size, a.size, 3)).to(dev, dt)
     x = x.contiguous(memory_format=torch.channels_last)
+    import threading
+    done = threading.Event()
+
+    def heartbeat():   # MIOpen compiles kernels on the first call; keep the run visibly alive
+        while not done.wait(30):
+            print(f"[miopen_baseline] still running ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
+    threading.Thread(target=heartbeat, daemon=True).start()
     with torch.no_grad():
         forward(p, x)        # first call: MIOpen kernel selection / compilation
         torch.cuda.synchronize()
@@ -52,6 +59,7 @@ def main():
             forward(p, x)
         torch.cuda.synchronize()
     dt_s = (time.perf_counter() - t0) / a.steps
+    done.set()
     print(json.dumps({"baseline": "pytorch-rocm eager (MIOpen)", "dtype": a.dtype, "batch": a.batch, "image": a.size,
                       "images_per_s": round(a.batch / dt_s, 2), "ms_per_step": round(1e3 * dt_s, 2),
                       "first_call_s": round(t_first, 1), "torch": torch.__version__}), flush=True)
