@@ -51,7 +51,7 @@ int ring_ns(int cfg) {
                                                                                          : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
 }
 int ring_tps(int cfg) { return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN) ? 3 : 1; }
-bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128; }
+bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128 || cfg == CFG_TRING_R64_NS4; }
 int cfg_limit() {
 #ifdef UNET_ABLATION
   return CFG_COUNT + 15;
@@ -1231,10 +1231,9 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
   constexpr int WI = BR / (16 * NW);          // A DMA instructions per wave and step
   constexpr int BI = 256 / (16 * NW);         // B DMA instructions per wave and step
   constexpr int ASLOT = BR * 64, BSLOT = 256 * 64, SLOT = ASLOT + BSLOT;
-  constexpr int PARAM_OFF = NS * SLOT;
-  static_assert(NS == 3 && TC % 4 == 0, "ring depth / row tile");
-  __shared__ __attribute__((aligned(16))) char lds[PARAM_OFF + BR * 4];
-  float* bias_s = reinterpret_cast<float*>(lds + PARAM_OFF);
+  static_assert((NS == 3 || NS == 4) && TC % 4 == 0, "ring depth / row tile");
+  static_assert(NS * SLOT <= 160 * 1024 / 2, "two blocks per CU");
+  __shared__ __attribute__((aligned(16))) char lds[NS * SLOT];   // the epilogue reads the bias from global (L2)
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   int bid;
@@ -1298,14 +1297,17 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
   }
   const int wrow = col * 64 + ((q ^ ((col >> 1) & 3)) << 4);
 
-  issue(0);
-  if (total > 1) issue(1);
-  for (int i = tid; i < BR; i += 256) bias_s[i] = a.bias[ct * BR + i];
-  if (total > 1) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (k < total) issue(k);
+  {   // step 0 landed; steps 1 .. NS-2 may stay in flight
+    const int young = total - 1 < NS - 2 ? total - 1 : NS - 2;
+    if (young == 2) wait_vm_barrier<2 * (WI + BI)>(); else if (young == 1) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
+  }
 
   int c = 0, item = 0;
   for (int g = 0; g < total; ++g) {
-    if (g + 2 < total) issue(g + 2);
+    if (g + NS - 1 < total) issue(g + NS - 1);
     const char* As = lds + (g % NS) * SLOT + wrow;
     const char* Bs = lds + (g % NS) * SLOT + ASLOT;
     frag_t bq[TP], ar[3];
@@ -1325,7 +1327,11 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
       __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
     }
     // step g+1 must have landed; step g+2 (issued above) may stay in flight
-    if (g + 2 < total) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
+    {   // step g+1 landed; steps g+2 .. g+NS-1 (issued) may stay in flight
+      int young = total - 2 - g;
+      young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
+      if (young == 2) wait_vm_barrier<2 * (WI + BI)>(); else if (young == 1) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
+    }
     if (++c == S) {
       c = 0;
       int n, ty, tx;
@@ -1333,7 +1339,8 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
         conv_epilogue<T, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
-                                            tx * 16, wave * TP, ct * BR + 64 * h, bias_s + 64 * h, nullptr, nullptr);
+                                            tx * 16, wave * TP, ct * BR + 64 * h, a.bias + ct * BR + 64 * h, nullptr,
+                                            nullptr);
 #pragma unroll
       for (int t = 0; t < TC; ++t)
 #pragma unroll
@@ -1345,7 +1352,7 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
 
 template <typename T, int TCW, int NS>
 static hipError_t launch_tring(const IgemmArgs& a, hipStream_t s) {
-  constexpr int BR = 16 * TCW, LDS = NS * (BR * 64 + 256 * 64) + BR * 4;
+  constexpr int BR = 16 * TCW, LDS = NS * (BR * 64 + 256 * 64);
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
   if (a.Cin % (64 / (int)sizeof(T)) || a.Ctot % BR || a.n_ct != a.Ctot / BR) return hipErrorInvalidValue;
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
@@ -1610,6 +1617,7 @@ static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipSt
       case CFG_HALO3_R64_W8: return launch_halo<T, 1, 8, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_HALO3_R64_W4: return launch_halo<T, 1, 4, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_TRING_R128: return launch_tring<T, 8, 3>(a, s);
+      case CFG_TRING_R64_NS4: return launch_tring<T, 4, 4>(a, s);
       default: return launch_cfg<T, 1, EPI_UPSCATTER>(cfg, a, s);
     }
   }
