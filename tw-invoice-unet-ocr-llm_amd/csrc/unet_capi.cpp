@@ -372,8 +372,7 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
   if (cfg >= CFG_COUNT) {
     std::snprintf(buf, sizeof buf, "ablation_%d<%s, %d>", cfg - CFG_COUNT, tname(t), epi);
   } else if (cfg_is_tring(cfg)) {
-    std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, %d, %d>", tname(t), cfg_rows(cfg) / 16,
-                  cfg == CFG_TRING_R64_NS4 ? 4 : 3);
+    std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, 3>", tname(t));
   } else if (cfg_is_ring(cfg)) {
     const int tc = cfg_rows(cfg) / 16;
     std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, 0, %d, %d>", tname(t), tc, ring_ns(cfg),
@@ -538,7 +537,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
                                   c == CFG_HALO1_R128T8_NS2 || c == CFG_HALO_R128_W8 || c == CFG_HALO1_R64_W8 ||
                                   c == CFG_HALO1_R128T8_NS3 || c == CFG_HALO_R128_W4 || c == CFG_HALO3_R64_W8 ||
                                   c == CFG_HALO3_R64_W4 || c == CFG_SG_R128T8_NS2 || c == CFG_SG_R64_W4 ||
-                                  c == CFG_TRING_R128 || c == CFG_TRING_R64_NS4))
+                                  c == CFG_TRING_R128))
           h->U[li].cfg = c;
       }
       pos = end + 1;

@@ -94,9 +94,7 @@ enum Cfg : int {
   CFG_TRING_R128 = 32,
   // down1.0 fused into down1.3 on the 3-taps-per-step ring (halo chunks computed from the input)
   CFG_RING_FUSED_IN = 33,
-  // ConvTranspose ring with 64-row tiles and a 4-slot ring (3 steps of prefetch)
-  CFG_TRING_R64_NS4 = 34,
-  CFG_COUNT = 35
+  CFG_COUNT = 34
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);

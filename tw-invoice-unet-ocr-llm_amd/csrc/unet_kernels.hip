@@ -51,7 +51,7 @@ int ring_ns(int cfg) {
                                                                                          : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
 }
 int ring_tps(int cfg) { return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN) ? 3 : 1; }
-bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128 || cfg == CFG_TRING_R64_NS4; }
+bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128; }
 int cfg_limit() {
 #ifdef UNET_ABLATION
   return CFG_COUNT + 15;
@@ -1617,7 +1617,6 @@ static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipSt
       case CFG_HALO3_R64_W8: return launch_halo<T, 1, 8, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_HALO3_R64_W4: return launch_halo<T, 1, 4, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_TRING_R128: return launch_tring<T, 8, 3>(a, s);
-      case CFG_TRING_R64_NS4: return launch_tring<T, 4, 4>(a, s);
       default: return launch_cfg<T, 1, EPI_UPSCATTER>(cfg, a, s);
     }
   }

@@ -140,3 +140,30 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
     m = m[0].cpu().numpy().astype(bool)
     masks = {k: m[i] for i, k in enumerate(FIELDS)}
     return masks, boxes_to_crops(pil_img, boxes[0].cpu().numpy())
+
+
+def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = None):
+    """Batched run_unet for serving: N photos -> [(masks, crops)] in order, identical per photo
+    to ``run_unet`` (same preprocessing, forward, masks, boxes and crop rules), but one native
+    forward over the whole batch.  RGB / L photos are resized on the GPU straight into their
+    slot of the batch input; other PIL modes take the reference's host resize."""
+    model = _cached_model(checkpoint_path, compute_dtype)
+    pil_imgs = list(pil_imgs)
+    if not pil_imgs:
+        return []
+    x = torch.empty((len(pil_imgs), 3, IMG_SIZE, IMG_SIZE), dtype=torch.float32, device=DEVICE)
+    for i, pil in enumerate(pil_imgs):
+        if pil.mode in ("RGB", "L") and str(DEVICE).startswith("cuda"):
+            img = torch.from_numpy(np.ascontiguousarray(np.asarray(pil))).to(DEVICE)
+            model.preprocess(img, IMG_SIZE, out=x[i])
+        else:
+            x[i] = preprocess(pil.resize((IMG_SIZE, IMG_SIZE)))[0]
+    with torch.no_grad():
+        m, boxes = model.forward_boxes(x, masks="u8")
+    m = m.cpu().numpy().astype(bool)
+    boxes = boxes.cpu().numpy()
+    out = []
+    for i, pil in enumerate(pil_imgs):
+        masks = {k: m[i, j] for j, k in enumerate(FIELDS)}
+        out.append((masks, boxes_to_crops(pil, boxes[i])))
+    return out
