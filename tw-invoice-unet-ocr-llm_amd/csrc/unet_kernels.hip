@@ -945,7 +945,8 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
   static_assert(WI >= 1 && BR % (G::RPI * NW) == 0, "weight tile split");
   static_assert(TP >= 1 && 16 % WPX == 0, "pixel groups per wave");
   static_assert(EPI != EPI_HEAD || BR == 64, "fused head needs the 64 channels in one block");
-  static_assert(HS == 0 || (sizeof(T) == 2 && BR == 64 && NW == 4 && EPI != EPI_HEAD), "fused first conv: 16-bit, 64 rows");
+  static_assert(HS == 0 || (sizeof(T) == 2 && BR == 64 && NW == 4 && TPS == 3 && EPI != EPI_HEAD),
+                "fused first conv: 16-bit, 64 rows, 3 taps per step");
   static_assert(WR * WPX >= 8 || G::LDS_BYTES <= 160 * 1024 / 2, "two blocks per CU");
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
   float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
@@ -1078,14 +1079,22 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       xoff[j] = k < 9 * a.c0 ? ((r / 3) * 20 + (r - (r / 3) * 3)) * 4 + c : -1;
     }
   }
-  auto compute_halo = [&](int i, int cb, int hb) {
+  // part = 0 / 1: the even / odd pixel groups of this wave (the chunk is computed over two
+  // steps, so that no single step carries all of it); at most 3 groups per part, unrolled so
+  // that the gathers of all of them are in flight together
+  constexpr int HGR = (kRingPix + 15) / 16;               // 16-pixel groups of the halo
+  constexpr int HIT = (HGR + 2 * NW - 1) / (2 * NW);      // groups per wave and part
+  auto compute_halo = [&](int i, int cb, int hb, int part) {
     if constexpr (HS != 0) {
       int n, ty, tx;
       tile_of(i, n, ty, tx);
       const T* xs = reinterpret_cast<const T*>(lds + G::XS_OFF);
       char* dst = lds + hb * HALO_BYTES;
       const int qq = lane >> 4;
-      for (int grp = wave; grp * 16 < kRingPix; grp += NW) {
+#pragma unroll
+      for (int it = 0; it < HIT; ++it) {
+        const int grp = wave + part * NW + it * 2 * NW;
+        if (grp >= HGR) break;   // wave-uniform
         const int p = grp * 16 + (lane & 15);
         const bool real = p < kRingPix;
         const int hy = real ? p / 18 : 0, hx = real ? p - (p / 18) * 18 : 0;
@@ -1117,7 +1126,8 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
   if constexpr (HS != 0) {
     issue_xs(0);
     wait_vm_barrier<0>();
-    compute_halo(0, 0, 0);
+    compute_halo(0, 0, 0, 0);
+    compute_halo(0, 0, 0, 1);
   } else {
     issue_halo(0);
   }
@@ -1167,15 +1177,18 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
     if (g + NS - 1 < total) issue_w(g + NS - 1);
     if constexpr (HS != 0) {
       // the next tile's window, once this tile's last halo chunk has been computed from it (at
-      // chunk 0, step 0; the barrier after that step retired every read of xs).  Issued after
-      // this step's weights, so the wait at the end of the NEXT step (for those weights) is the
-      // one that retires it: two steps of latency before chunk 1 computes the next tile's halo.
-      if (c == 0 && tap == 1 && item + 1 < items) issue_xs(item + 1);
+      // chunk 0, steps 0 and 1; the barrier after step 1 retired every read of xs).  Issued
+      // after this step's weights, so the wait at the end of the NEXT step (for those weights)
+      // is the one that retires it: chunk 1 computes the next tile's halo at its steps 1 and 2.
+      if (c == 0 && tap == 2 && item + 1 < items) issue_xs(item + 1);
     }
 #pragma unroll
     for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
-    if constexpr (HS != 0) {   // next chunk's halo into the other buffer (last read one step ago)
-      if (hnext) compute_halo(c + 1 < nch ? item : item + 1, c + 1 < nch ? c + 1 : 0, (hseq + 1) & 1);
+    if constexpr (HS != 0) {   // next chunk's halo into the other buffer (last read a chunk ago),
+      // in two halves: chunk 1 of this tile at steps 0, 1 of chunk 0; chunk 0 of the next tile
+      // at steps 1, 2 of chunk 1 (down1.3: Cin = 64, so nch = 2 and SPC = 3)
+      if (c == 0 && tap < 2) compute_halo(item, 1, (hseq + 1) & 1, tap);
+      else if (c == 1 && tap >= 1 && item + 1 < items) compute_halo(item + 1, 0, (hseq + 1) & 1, tap - 1);
     }
     // W(g+1) must have landed (and, at a chunk end, the next halo -- issued 8 steps earlier,
     // so older than W(g+1)).  Younger loads may stay in flight: W(g+2 .. g+NS-1) and a halo
