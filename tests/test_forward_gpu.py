@@ -208,7 +208,7 @@ def test_every_kernel_config(cfg, monkeypatch):
         m.close()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 4, 5, 8, 9, 14, 15, 21, 22, 32])
+@pytest.mark.parametrize("cfg", [0, 1, 4, 5, 8, 9, 14, 15, 21, 22, 32, 34])
 def test_convtranspose_configs(cfg, monkeypatch):
     """ConvTranspose2d (up4..up1) on every supported kernel configuration vs the golden."""
     monkeypatch.setenv("UNET_MI355X_UPCFG", ",".join(f"{i}:{cfg}" for i in range(4)))

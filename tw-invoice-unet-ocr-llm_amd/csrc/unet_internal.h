@@ -94,7 +94,9 @@ enum Cfg : int {
   CFG_TRING_R128 = 32,
   // down1.0 fused into down1.3 on the 3-taps-per-step ring (halo chunks computed from the input)
   CFG_RING_FUSED_IN = 33,
-  CFG_COUNT = 34
+  // ConvTranspose ring with the row tiles of one pixel tile taken back to back by one walker
+  CFG_TRING_R128_CTI = 34,
+  CFG_COUNT = 35
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);

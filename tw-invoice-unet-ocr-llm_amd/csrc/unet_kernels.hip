@@ -37,7 +37,8 @@ int cfg_rows(int cfg) {
   return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8 ||
           cfg == CFG_HALO1_R128_W4 || cfg == CFG_PHALO_R128_W8 || cfg == CFG_HALO1_R128T8_NS2 ||
           cfg == CFG_HALO1_R128T8_NS3 || cfg == CFG_SG_R128T8_NS2 || cfg == CFG_SG_R128T8_NS3 ||
-          cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3 || cfg == CFG_TRING_R128) ? 128 : 64;
+          cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3 || cfg == CFG_TRING_R128 ||
+          cfg == CFG_TRING_R128_CTI) ? 128 : 64;
 }
 bool cfg_single_chunk(int cfg) { (void)cfg; return false; }
 int cfg_pixels(int cfg) {
@@ -51,7 +52,7 @@ int ring_ns(int cfg) {
                                                                                          : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
 }
 int ring_tps(int cfg) { return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN) ? 3 : 1; }
-bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128; }
+bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128 || cfg == CFG_TRING_R128_CTI; }
 int cfg_limit() {
 #ifdef UNET_ABLATION
   return CFG_COUNT + 15;
@@ -1238,7 +1239,10 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
 // scatter epilogue.  LDS per slot: A [BR][64 B] (chunk q of row r at q ^ ((r >> 1) & 3)) +
 // B [256 px][64 B] (pixel row py*16+px, chunk q at q ^ ((py & 1) << 1): conflict-free for all
 // ds_read_b128 lane groups and pixel groups, checked exhaustively).
-template <typename T, int TCW, int NS>
+// CTI = 1: a walker takes the n_ct row tiles of one pixel tile back to back (the B tile of row
+// tile ct > 0 is then re-read from L2 right after row tile 0 read it from HBM) instead of one
+// walker per row tile.
+template <typename T, int TCW, int NS, int CTI = 0>
 __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
   constexpr int NW = 4, TC = TCW, TP = 4, BR = 16 * TC, BKE = 64 / (int)sizeof(T);
   constexpr int WI = BR / (16 * NW);          // A DMA instructions per wave and step
@@ -1255,22 +1259,24 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
     const int b = blockIdx.x, x = b & 7, k = b >> 3;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
   }
-  const int ct = bid % a.n_ct;
-  const int slot = bid / a.n_ct;
-  const int n_slots = gridDim.x / a.n_ct;
+  const int NCT = CTI ? a.n_ct : 1;                 // row tiles per pixel tile of one walker
+  const int ct0 = CTI ? 0 : bid % a.n_ct;
+  const int slot = CTI ? bid : bid / a.n_ct;
+  const int n_slots = CTI ? gridDim.x : gridDim.x / a.n_ct;
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
   if (slot >= n_mt) return;
-  const int items = (n_mt - slot + n_slots - 1) / n_slots;
+  const int items = NCT * ((n_mt - slot + n_slots - 1) / n_slots);
   const int H = a.H, W = a.W;
   const int S = a.Cin / BKE;
   const int total = items * S;
 
-  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * ASLOT +
+  const char* wblk = reinterpret_cast<const char*>(a.wgt) +
                      (wave * WI * 16 + (lane >> 2)) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
   const char* in = reinterpret_cast<const char*>(a.in);
   const char* zero = reinterpret_cast<const char*>(a.zero);
+  auto ct_of = [&](int i) { return CTI ? i - (i / NCT) * NCT : ct0; };
   auto tile_of = [&](int i, int& n, int& ty, int& tx) {
-    int mt = slot + i * n_slots;
+    int mt = slot + (CTI ? i / NCT : i) * n_slots;
     tx = mt % a.tiles_x;
     mt /= a.tiles_x;
     ty = mt % a.tiles_y;
@@ -1280,7 +1286,8 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
     const int i = g / S, c = g - (g / S) * S;
     char* As = lds + (g % NS) * SLOT;
 #pragma unroll
-    for (int j = 0; j < WI; ++j) glds16(wblk + (size_t)c * ASLOT + j * 1024, As + (wave * WI + j) * 1024);
+    for (int j = 0; j < WI; ++j)
+      glds16(wblk + ((size_t)ct_of(i) * S + c) * ASLOT + j * 1024, As + (wave * WI + j) * 1024);
     int n, ty, tx;
     tile_of(i, n, ty, tx);
 #pragma unroll
@@ -1349,6 +1356,7 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
       c = 0;
       int n, ty, tx;
       tile_of(item, n, ty, tx);
+      const int ct = ct_of(item);
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
         conv_epilogue<T, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
@@ -1363,16 +1371,17 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
   }
 }
 
-template <typename T, int TCW, int NS>
+template <typename T, int TCW, int NS, int CTI = 0>
 static hipError_t launch_tring(const IgemmArgs& a, hipStream_t s) {
   constexpr int BR = 16 * TCW, LDS = NS * (BR * 64 + 256 * 64);
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
   if (a.Cin % (64 / (int)sizeof(T)) || a.Ctot % BR || a.n_ct != a.Ctot / BR) return hipErrorInvalidValue;
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
-  int n_slots = (kNumCUs * ((160 * 1024) / LDS)) / a.n_ct;
+  const int nct = CTI ? 1 : a.n_ct;   // walkers per pixel-tile sequence
+  int n_slots = (kNumCUs * ((160 * 1024) / LDS)) / nct;
   if (n_slots < 1) n_slots = 1;
   if (n_slots > n_mt) n_slots = n_mt;
-  hipLaunchKernelGGL((convT_ring_kernel<T, TCW, NS>), dim3(a.n_ct * n_slots), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((convT_ring_kernel<T, TCW, NS, CTI>), dim3(nct * n_slots), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1630,6 +1639,7 @@ static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipSt
       case CFG_HALO3_R64_W8: return launch_halo<T, 1, 8, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_HALO3_R64_W4: return launch_halo<T, 1, 4, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_TRING_R128: return launch_tring<T, 8, 3>(a, s);
+      case CFG_TRING_R128_CTI: return launch_tring<T, 8, 3, 1>(a, s);
       default: return launch_cfg<T, 1, EPI_UPSCATTER>(cfg, a, s);
     }
   }
