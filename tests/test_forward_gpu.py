@@ -208,7 +208,7 @@ def test_every_kernel_config(cfg, monkeypatch):
         m.close()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 4, 5, 8, 9, 14, 15, 21, 22, 32, 34])
+@pytest.mark.parametrize("cfg", [0, 1, 4, 5, 8, 9, 14, 15, 21, 22, 32, 34, 35, 36])
 def test_convtranspose_configs(cfg, monkeypatch):
     """ConvTranspose2d (up4..up1) on every supported kernel configuration vs the golden."""
     monkeypatch.setenv("UNET_MI355X_UPCFG", ",".join(f"{i}:{cfg}" for i in range(4)))
@@ -274,7 +274,7 @@ def test_forward_deterministic_and_config_invariant(dtype, monkeypatch):
             d = _first_diff(_forced(cfg, None, sd, x, dtype, monkeypatch), fbase)
             if d:
                 bad.append((cfg, None, d[:3]))
-    for up in (4, 5, 8, 9, 14, 15, 21, 22, 23, 25, 32):
+    for up in (4, 5, 8, 9, 14, 15, 21, 22, 23, 25, 32, 34, 35, 36):
         d = _first_diff(_forced(None, up, sd, x, dtype, monkeypatch), base)
         if d:
             bad.append((None, up, d[:3]))

@@ -372,7 +372,8 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
   if (cfg >= CFG_COUNT) {
     std::snprintf(buf, sizeof buf, "ablation_%d<%s, %d>", cfg - CFG_COUNT, tname(t), epi);
   } else if (cfg_is_tring(cfg)) {
-    std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, 3, %d>", tname(t), cfg == CFG_TRING_R128_CTI ? 1 : 0);
+    std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, %d, %d, %d>", tname(t), cfg == CFG_TRING_R256_NS4 ? 4 : 3,
+                  cfg == CFG_TRING_R128_CTI ? 1 : 0, cfg == CFG_TRING_R256 || cfg == CFG_TRING_R256_NS4 ? 2 : 1);
   } else if (cfg_is_ring(cfg)) {
     const int tc = cfg_rows(cfg) / 16;
     std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, 0, %d, %d>", tname(t), tc, ring_ns(cfg),
@@ -521,7 +522,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     h->U[i].cout = kUpCh[i][1];
     h->U[i].ctot = 4 * kUpCh[i][1];
     h->U[i].taps = 1;
-    h->U[i].cfg = ps == "gather" ? CFG_R128_P128 : (cfg->dtype == UNET_DTYPE_F32 ? kDefaultUpCfg[i] : (i == 3 ? (int)CFG_TRING_R128_CTI : (int)CFG_TRING_R128));
+    h->U[i].cfg = ps == "gather" ? CFG_R128_P128 : (cfg->dtype == UNET_DTYPE_F32 ? kDefaultUpCfg[i] : (int)CFG_TRING_R256_NS4);
   }
   if (const char* ov = std::getenv("UNET_MI355X_UPCFG")) {   // "i:cfg,..." i = 0..3 (up4..up1)
     std::string o(ov);
@@ -537,7 +538,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
                                   c == CFG_HALO1_R128T8_NS2 || c == CFG_HALO_R128_W8 || c == CFG_HALO1_R64_W8 ||
                                   c == CFG_HALO1_R128T8_NS3 || c == CFG_HALO_R128_W4 || c == CFG_HALO3_R64_W8 ||
                                   c == CFG_HALO3_R64_W4 || c == CFG_SG_R128T8_NS2 || c == CFG_SG_R64_W4 ||
-                                  c == CFG_TRING_R128 || c == CFG_TRING_R128_CTI))
+                                  c == CFG_TRING_R128 || c == CFG_TRING_R128_CTI || c == CFG_TRING_R256 ||
+                                  c == CFG_TRING_R256_NS4))
           h->U[li].cfg = c;
       }
       pos = end + 1;

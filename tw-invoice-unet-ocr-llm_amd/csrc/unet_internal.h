@@ -96,7 +96,9 @@ enum Cfg : int {
   CFG_RING_FUSED_IN = 33,
   // ConvTranspose ring with the row tiles of one pixel tile taken back to back by one walker
   CFG_TRING_R128_CTI = 34,
-  CFG_COUNT = 35
+  // ConvTranspose ring with 8-wave 256-row x 256-pixel block tiles (one block per CU)
+  CFG_TRING_R256 = 35, CFG_TRING_R256_NS4 = 36,
+  CFG_COUNT = 37
 };
 bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);

@@ -38,7 +38,7 @@ int cfg_rows(int cfg) {
           cfg == CFG_HALO1_R128_W4 || cfg == CFG_PHALO_R128_W8 || cfg == CFG_HALO1_R128T8_NS2 ||
           cfg == CFG_HALO1_R128T8_NS3 || cfg == CFG_SG_R128T8_NS2 || cfg == CFG_SG_R128T8_NS3 ||
           cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3 || cfg == CFG_TRING_R128 ||
-          cfg == CFG_TRING_R128_CTI) ? 128 : 64;
+          cfg == CFG_TRING_R128_CTI) ? 128 : (cfg == CFG_TRING_R256 || cfg == CFG_TRING_R256_NS4 ? 256 : 64);
 }
 bool cfg_single_chunk(int cfg) { (void)cfg; return false; }
 int cfg_pixels(int cfg) {
@@ -52,7 +52,9 @@ int ring_ns(int cfg) {
                                                                                          : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
 }
 int ring_tps(int cfg) { return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN) ? 3 : 1; }
-bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128 || cfg == CFG_TRING_R128_CTI; }
+bool cfg_is_tring(int cfg) {
+  return cfg == CFG_TRING_R128 || cfg == CFG_TRING_R128_CTI || cfg == CFG_TRING_R256 || cfg == CFG_TRING_R256_NS4;
+}
 int cfg_limit() {
 #ifdef UNET_ABLATION
   return CFG_COUNT + 15;
@@ -1241,18 +1243,21 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
 // ds_read_b128 lane groups and pixel groups, checked exhaustively).
 // CTI = 1: a walker takes the n_ct row tiles of one pixel tile back to back (the B tile of row
 // tile ct > 0 is then re-read from L2 right after row tile 0 read it from HBM) instead of one
-// walker per row tile.
-template <typename T, int TCW, int NS, int CTI = 0>
-__global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
-  constexpr int NW = 4, TC = TCW, TP = 4, BR = 16 * TC, BKE = 64 / (int)sizeof(T);
+// walker per row tile.  WRW = 2: 8 waves as 2 (rows) x 4 (pixels), a 256-row x 256-pixel block
+// tile (one block per CU): half the A + B LDS-DMA bytes per MFMA of the 128-row tile (the
+// large-Cin layers up4/up3 stream both operands from L2 at every step).
+template <typename T, int TCW, int NS, int CTI = 0, int WRW = 1>
+__global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel(const IgemmArgs a) {
+  constexpr int NW = 4 * WRW, TC = TCW, TP = 4, BR = 16 * TC * WRW, BKE = 64 / (int)sizeof(T);
   constexpr int WI = BR / (16 * NW);          // A DMA instructions per wave and step
   constexpr int BI = 256 / (16 * NW);         // B DMA instructions per wave and step
   constexpr int ASLOT = BR * 64, BSLOT = 256 * 64, SLOT = ASLOT + BSLOT;
   static_assert((NS == 3 || NS == 4) && TC % 4 == 0, "ring depth / row tile");
-  static_assert(NS * SLOT <= 160 * 1024 / 2, "two blocks per CU");
+  static_assert(NS * SLOT <= 160 * 1024 / (WRW == 1 ? 2 : 1), "blocks per CU");
   __shared__ __attribute__((aligned(16))) char lds[NS * SLOT];   // the epilogue reads the bias from global (L2)
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 2, wp = wave & 3;   // row group (WRW = 2), pixel group
   int bid;
   {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one walker
     const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
@@ -1312,10 +1317,10 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
 #pragma unroll
   for (int p = 0; p < TP; ++p) {
     int py, px;
-    pix_of((wave * TP + p) * 16 + col, py, px);
+    pix_of((wp * TP + p) * 16 + col, py, px);
     prow[p] = (py * 16 + px) * 64 + ((q ^ ((py & 1) << 1)) << 4);
   }
-  const int wrow = col * 64 + ((q ^ ((col >> 1) & 3)) << 4);
+  const int wrow = (wr * 16 * TC + col) * 64 + ((q ^ ((col >> 1) & 3)) << 4);
 
 #pragma unroll
   for (int k = 0; k < NS - 1; ++k)
@@ -1360,7 +1365,8 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
         conv_epilogue<T, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
-                                            tx * 16, wave * TP, ct * BR + 64 * h, a.bias + ct * BR + 64 * h, nullptr,
+                                            tx * 16, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
+                                            a.bias + ct * BR + wr * 16 * TC + 64 * h, nullptr,
                                             nullptr);
 #pragma unroll
       for (int t = 0; t < TC; ++t)
@@ -1371,9 +1377,9 @@ __global__ __launch_bounds__(256, 2) void convT_ring_kernel(const IgemmArgs a) {
   }
 }
 
-template <typename T, int TCW, int NS, int CTI = 0>
+template <typename T, int TCW, int NS, int CTI = 0, int WRW = 1>
 static hipError_t launch_tring(const IgemmArgs& a, hipStream_t s) {
-  constexpr int BR = 16 * TCW, LDS = NS * (BR * 64 + 256 * 64);
+  constexpr int BR = 16 * TCW * WRW, LDS = NS * (BR * 64 + 256 * 64);
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
   if (a.Cin % (64 / (int)sizeof(T)) || a.Ctot % BR || a.n_ct != a.Ctot / BR) return hipErrorInvalidValue;
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
@@ -1381,7 +1387,7 @@ static hipError_t launch_tring(const IgemmArgs& a, hipStream_t s) {
   int n_slots = (kNumCUs * ((160 * 1024) / LDS)) / nct;
   if (n_slots < 1) n_slots = 1;
   if (n_slots > n_mt) n_slots = n_mt;
-  hipLaunchKernelGGL((convT_ring_kernel<T, TCW, NS, CTI>), dim3(nct * n_slots), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((convT_ring_kernel<T, TCW, NS, CTI, WRW>), dim3(nct * n_slots), dim3(256 * WRW), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1640,6 +1646,8 @@ static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipSt
       case CFG_HALO3_R64_W4: return launch_halo<T, 1, 4, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
       case CFG_TRING_R128: return launch_tring<T, 8, 3>(a, s);
       case CFG_TRING_R128_CTI: return launch_tring<T, 8, 3, 1>(a, s);
+      case CFG_TRING_R256: return launch_tring<T, 8, 3, 0, 2>(a, s);
+      case CFG_TRING_R256_NS4: return launch_tring<T, 8, 4, 0, 2>(a, s);
       default: return launch_cfg<T, 1, EPI_UPSCATTER>(cfg, a, s);
     }
   }
