@@ -6,20 +6,23 @@ HBM: UNet(3,3) forward at 512x512 (unet_model.py:55-86) with the fused sigmoid +
 per-field threshold (inference.py:72-79) producing bit-packed masks, plus -- for N>1 --
 the RCCL all-gather of the masks over xGMI.  Per-GPU batch is fixed (weak scaling).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--dtype bf16]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--dtype mixed]
     torchrun --nproc-per-node N bench.py --gpus N ...      (the driver does this for N>1)
 
 Rank 0 prints ONE JSON line.  Extra fields: roofline (dominant kernel, HIP-event timed
-inside this run), cpu_baseline (the oracle on this host's cores, bounded sample, with
-mask IoU of the GPU masks against it), kernels (per-instantiation time breakdown).
+inside this run), cpu_baseline (the oracle on this host's cores, bounded sample: batch-1 and
+batch-8 forward, run_unet end to end with its model load, and the mask IoU of the GPU masks
+against the CPU masks), latency_bs1 (the drop-in run_unet and the batch-1 forward, eager and
+hipGraph), kernels (per-instantiation time breakdown).
 """
 from __future__ import annotations
 
 import argparse
-import re
 import json
 import os
+import re
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -31,56 +34,67 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from unet_mi355x import native  # noqa: E402
-from unet_mi355x.dist import all_gather_rows  # noqa: E402
+from unet_mi355x import dist as udist  # noqa: E402
 from unet_mi355x import synthetic as syn  # noqa: E402
 from unet_mi355x.model import UNet  # noqa: E402
 
 METRIC = "invoice masks/sec at 512x512 bs256, 1/2/4/8 MI355X; IoU vs CPU ref"
-PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA (MI355X_MICROARCH.md)
-PEAK_HBM_GBS = 8000.0
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "mixed": 2500.0, "fp32": 157.3}   # dense MFMA (MI355X_MICROARCH.md)
+PLAN = {"mixed": "bf16 storage at resolution levels 2-4 (64..1024 ch, 128^2..32^2), fp16 at levels 0-1 "
+                 "(512^2, 256^2); fp32 accumulation, fp32 head",
+        "bf16": "bf16 storage, fp32 accumulation, fp32 head", "fp16": "fp16 storage, fp32 accumulation, fp32 head",
+        "fp32": "fp32 (exact-fp32 MFMA)"}
 
-# launch order of include/unet_mi355x.h: (name, layer group, cin, cout, level, kind); the
-# kernel instantiation of each launch comes from the library (unet_launch_label)
+# launch order of include/unet_mi355x.h: (name, cin, cout, input level, kind); the kernel
+# instantiation of each launch comes from the library (unet_launch_label)
 LAUNCHES = [
-    ("down1.0", "first_conv", None, 64, 0, "first"),
-    ("down1.3", "igemm_r64p256_pool", 64, 64, 0, "c3"),
-    ("down2.0", "igemm_r128p128_store", 64, 128, 1, "c3"),
-    ("down2.3", "igemm_r128p128_pool", 128, 128, 1, "c3"),
-    ("down3.0", "igemm_r128p128_store", 128, 256, 2, "c3"),
-    ("down3.3", "igemm_r128p128_pool", 256, 256, 2, "c3"),
-    ("down4.0", "igemm_r128p128_store", 256, 512, 3, "c3"),
-    ("down4.3", "igemm_r128p128_pool", 512, 512, 3, "c3"),
-    ("bottleneck.0", "igemm_r128p128_store", 512, 1024, 4, "c3"),
-    ("bottleneck.3", "igemm_r128p128_store", 1024, 1024, 4, "c3"),
-    ("up4", "igemm_r128p128_upscatter", 1024, 512, 4, "up"),
-    ("conv4.0", "igemm_r128p128_store", 1024, 512, 3, "c3"),
-    ("conv4.3", "igemm_r128p128_store", 512, 512, 3, "c3"),
-    ("up3", "igemm_r128p128_upscatter", 512, 256, 3, "up"),
-    ("conv3.0", "igemm_r128p128_store", 512, 256, 2, "c3"),
-    ("conv3.3", "igemm_r128p128_store", 256, 256, 2, "c3"),
-    ("up2", "igemm_r128p128_upscatter", 256, 128, 2, "up"),
-    ("conv2.0", "igemm_r128p128_store", 256, 128, 1, "c3"),
-    ("conv2.3", "igemm_r128p128_store", 128, 128, 1, "c3"),
-    ("up1", "igemm_r128p128_upscatter", 128, 64, 1, "up"),
-    ("conv1.0", "igemm_r64p256_store", 128, 64, 0, "c3"),
-    ("conv1.3", "igemm_r64p128_head", 64, 64, 0, "c3"),
+    ("down1.0", None, 64, 0, "first"),
+    ("down1.3", 64, 64, 0, "c3"),
+    ("down2.0", 64, 128, 1, "c3"),
+    ("down2.3", 128, 128, 1, "c3"),
+    ("down3.0", 128, 256, 2, "c3"),
+    ("down3.3", 256, 256, 2, "c3"),
+    ("down4.0", 256, 512, 3, "c3"),
+    ("down4.3", 512, 512, 3, "c3"),
+    ("bottleneck.0", 512, 1024, 4, "c3"),
+    ("bottleneck.3", 1024, 1024, 4, "c3"),
+    ("up4", 1024, 512, 4, "up"),
+    ("conv4.0", 1024, 512, 3, "c3"),
+    ("conv4.3", 512, 512, 3, "c3"),
+    ("up3", 512, 256, 3, "up"),
+    ("conv3.0", 512, 256, 2, "c3"),
+    ("conv3.3", 256, 256, 2, "c3"),
+    ("up2", 256, 128, 2, "up"),
+    ("conv2.0", 256, 128, 1, "c3"),
+    ("conv2.3", 128, 128, 1, "c3"),
+    ("up1", 128, 64, 1, "up"),
+    ("conv1.0", 128, 64, 0, "c3"),
+    ("conv1.3", 64, 64, 0, "c3"),
 ]
 TYPE_CODE = {"float": "f", "__bf16": "DF16b", "_Float16": "DF16_"}
 
 
 def mangled(label):
-    """Itanium-mangled symbol of a "kernel<T, ints...>" label (what rocprofv3 may print)."""
-    m = re.match(r"(\w+)<([\w]+), ([\d, ]+)>$", label)
+    """Itanium-mangled symbol of a "kernel<args>" label (what rocprofv3 may print): template
+    arguments are element types or ints, the kernel takes one IgemmArgs."""
+    m = re.match(r"(\w+)<(.+)>$", label)
     if not m:
         return None
-    name, t, ints = m.group(1), m.group(2), [int(v) for v in m.group(3).split(", ")]
-    args = "".join(f"Li{v}E" for v in ints)
-    return f"_ZN4unet{len(name)}{name}I{TYPE_CODE[t]}{args}EEvNS_9IgemmArgsE"
+    args = ""
+    for tok in (t.strip() for t in m.group(2).split(",")):
+        if tok in TYPE_CODE:
+            args += TYPE_CODE[tok]
+        elif re.fullmatch(r"-?\d+", tok):
+            args += f"Li{tok}E"
+        else:
+            return None
+    name = m.group(1)
+    return f"_ZN4unet{len(name)}{name}I{args}EEvNS_9IgemmArgsE"
 
 
 def launch_flops(entry, n, h, w, c_in, ncls=3):
     """Algorithmic FLOPs (2 per MAC) of one launch over n images of h x w."""
-    name, _, cin, cout, lvl, kind = entry
+    name, cin, cout, lvl, kind = entry
     hh, ww = h >> lvl, w >> lvl
     if kind == "first":
         return 2.0 * 9 * c_in * cout * hh * ww * n
@@ -95,7 +109,7 @@ def launch_flops(entry, n, h, w, c_in, ncls=3):
 def launch_bytes(entry, n, h, w, c_in, esize, ncls=3):
     """Algorithmic HBM bytes of one launch: every activation read once and written once,
     weights read once, concat zero-copy, BN/ReLU/pool/head fused."""
-    name, _, cin, cout, lvl, kind = entry
+    name, cin, cout, lvl, kind = entry
     hh, ww = h >> lvl, w >> lvl
     if kind == "first":
         return n * c_in * hh * ww * 4 + n * hh * ww * cout * esize + 9 * c_in * 64 * 4
@@ -118,6 +132,132 @@ def gen_pages(seed, batch, size, channels, unique=32):
     return np.ascontiguousarray(np.concatenate([pages] * reps, axis=0)[:batch])
 
 
+def host_cores():
+    """(threads to use, description) of this host's CPU share: the affinity mask, capped by the
+    cgroup CPU quota when one is set (on the GPU box os.cpu_count() shows the whole machine)."""
+    total = os.cpu_count() or 1
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    use = min(avail, quota) if quota else avail
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return use, {"os_cpu_count": total, "affinity": avail, "cgroup_quota": quota, "cpu_model": model}
+
+
+def cpu_baseline(args, model, x, masks, C, S):
+    """The oracle (fp32 eager torch restating unet_model.py / inference.py) on this host's
+    cores: batch-1 forward (images/s + the mask IoU of the GPU masks), batch-8 forward, and
+    run_unet end to end (model load + resize + forward + masks + crops, inference.py:50-129)."""
+    from PIL import Image
+    from oracle import unet_oracle as orc
+    threads, info = host_cores()
+    torch.set_num_threads(threads)
+    sd_cpu = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    xc = x[:64].cpu()
+    mk = np.unpackbits(masks[:64].cpu().numpy(), axis=-1, bitorder="little").astype(bool)
+    orc.unet_forward(sd_cpu, xc[:1, :, :64, :64])  # warm the CPU kernels
+    done, ious, t0 = 0, [], time.perf_counter()
+    while done < xc.shape[0] and (done == 0 or time.perf_counter() - t0 < args.cpu_seconds):
+        lg = orc.unet_forward(sd_cpu, xc[done:done + 1]).numpy()[0]
+        ref = orc.masks_from_logits(lg)
+        ious += [orc.mask_iou(mk[done, i], ref[f]) for i, f in enumerate(orc.FIELDS)]
+        done += 1
+    t_bs1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    orc.unet_forward(sd_cpu, xc[:8])
+    t_bs8 = time.perf_counter() - t0
+    # run_unet on a 600x400 photo, checkpoint re-loaded on every call as the reference does
+    page = syn.invoice_pages(7, 1, 400, 600, 1)[0, 0]
+    pil = Image.fromarray((np.stack([page, page * 0.97, page * 0.94], -1) * 255 + 0.5).astype(np.uint8), "RGB")
+    with tempfile.TemporaryDirectory() as td:
+        ck = os.path.join(td, "best_unet_model.pth")
+        torch.save(sd_cpu, ck)
+        lat = []
+        for _ in range(2):
+            t0 = time.perf_counter()
+            orc.run_unet(pil, ck)
+            lat.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        orc.load_model_state(ck)
+        t_load = time.perf_counter() - t0
+    return {"value": round(done / t_bs1, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{done} of the bench images, batch 1, {S}x{S}, fp32 eager torch (oracle/unet_oracle.py), "
+                      f"{threads} threads",
+            "host": info,
+            "bs8_images_per_s": round(8 / t_bs8, 4),
+            "run_unet_s": round(float(np.median(lat)), 3), "model_load_s": round(t_load, 3),
+            "run_unet_sample": "600x400 RGB photo, 2 calls, checkpoint re-loaded per call (inference.py:58)",
+            "iou_vs_cpu": {"min": round(min(ious), 5), "mean": round(float(np.mean(ious)), 5),
+                           "images": done, "gpu_dtype": args.dtype}}
+
+
+def gpu_latency(args, model, dev):
+    """Batch-1 latency on the GPU: the drop-in run_unet (cached model, GPU preprocessing,
+    fused masks + boxes, host crops; inference.py:50-129) and the bare batch-1 forward,
+    eager (22 launches from the host) and as one hipGraph replay (unet_graph_launch)."""
+    from PIL import Image
+    from unet_mi355x import inference as inf
+    out = {}
+    page = syn.invoice_pages(7, 1, 400, 600, 1)[0, 0]
+    pil = Image.fromarray((np.stack([page, page * 0.97, page * 0.94], -1) * 255 + 0.5).astype(np.uint8), "RGB")
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    inf.DEVICE = str(dev)
+    with tempfile.TemporaryDirectory() as td:
+        ck = os.path.join(td, "best_unet_model.pth")
+        torch.save(sd, ck)
+        t0 = time.perf_counter()
+        inf.run_unet(pil, ck, compute_dtype=args.dtype)
+        out["run_unet_first_call_ms"] = round(1e3 * (time.perf_counter() - t0), 2)
+        lat = []
+        for _ in range(20):
+            t0 = time.perf_counter()
+            inf.run_unet(pil, ck, compute_dtype=args.dtype)
+            lat.append(time.perf_counter() - t0)
+        out["run_unet_ms"] = round(1e3 * float(np.median(lat)), 3)
+    h = model.native_handle(dev)
+    x1 = torch.from_numpy(gen_pages(3, 1, 512, 3)).to(dev)
+    m1 = torch.empty((1, 3, 512, 64), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    h.reserve(1, 512, 512)
+    for _ in range(3):
+        h.forward(x1, None, m1, native.MASK_BITS, stream)
+    torch.cuda.synchronize()
+    ref = m1.clone()
+    reps = 50
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        h.forward(x1, None, m1, native.MASK_BITS, stream)
+    e1.record()
+    torch.cuda.synchronize()
+    out["forward_bs1_eager_ms"] = round(e0.elapsed_time(e1) / reps, 4)
+    g = h.graph(x1, None, m1, native.MASK_BITS)
+    m1.zero_()
+    g.launch(stream)
+    torch.cuda.synchronize()
+    out["graph_matches_eager"] = bool(torch.equal(m1, ref))
+    e0.record()
+    for _ in range(reps):
+        g.launch(stream)
+    e1.record()
+    torch.cuda.synchronize()
+    out["forward_bs1_graph_ms"] = round(e0.elapsed_time(e1) / reps, 4)
+    g.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -126,10 +266,11 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--channels", type=int, default=3)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--dtype", default="mixed", choices=["mixed", "bf16", "fp16", "fp32"])
     ap.add_argument("--weights", default="pretrained", choices=["pretrained", "structured"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-layer-profile", action="store_true")
     ap.add_argument("--traffic-json", default="auto",
                     help="PMC summary (tools/pmc_summary.py output) to fill roofline.traffic; 'auto' = "
@@ -175,30 +316,28 @@ def main():
     masks = torch.empty((B, 3, S, S // 8), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    def segment(x_local, masks_local):
+        handle.forward(x_local, None, masks_local, native.MASK_BITS, stream)
+
     def step():
-        handle.forward(x, None, masks, native.MASK_BITS, stream)
-        if world > 1:   # the one exchange step: RCCL all-gather of the bit-packed masks
-            all_gather_rows(masks, world * B)
+        if world > 1:   # this rank's shard + the one exchange step: RCCL all-gather of the masks
+            udist.sharded_mask_step(segment, x, masks, world * B)
+        else:
+            segment(x, masks)
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]   # per-step spread (diagnostic)
+    marks = iter(ev[1:])
+
+    def timed_step():
+        step()
+        e = next(marks, None)
+        if e is not None:
+            e.record()
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]   # per-step spread (diagnostic)
-    t0 = time.perf_counter()
     ev[0].record()
-    for i in range(args.steps):
-        step()
-        ev[i + 1].record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, _ = udist.timed_steps(timed_step, args.steps, 0, sync=torch.cuda.synchronize, device=dev)
     ms_per_step = 1e3 * elapsed / args.steps
     step_ms = [round(ev[i].elapsed_time(ev[i + 1]), 3) for i in range(args.steps)]
     value = world * B * args.steps / elapsed
@@ -240,42 +379,32 @@ def main():
                     "frac": round(achieved / peak, 4), "traffic": traffic,
                     "launches_per_step": dom["launches"], "avg_launch_ms": dom["avg_launch_ms"],
                     "gflop_per_launch": round(dom["gflop"] / dom["launches"], 1),
+                    "algo_bytes_per_launch": round(dom["algo_gb"] * 1e9 / dom["launches"]),
                     "whole_step_tflops": round(sum(launch_flops(e, B, S, S, C) for e in LAUNCHES) / 1e9 /
                                                sum(ms), 1)}
 
     # ---- CPU baseline (the oracle, fp32 eager on this host), rank 0 at N=1 only
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import unet_oracle as orc
-        sd_cpu = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-        nthreads = torch.get_num_threads()
-        xc = x[:64].cpu()
-        mk = np.unpackbits(masks[:64].cpu().numpy(), axis=-1, bitorder="little").astype(bool)
-        orc.unet_forward(sd_cpu, xc[:1, :, :64, :64])  # warm the CPU kernels
-        done, ious, t0 = 0, [], time.perf_counter()
-        while done < xc.shape[0] and (done == 0 or time.perf_counter() - t0 < args.cpu_seconds):
-            lg = orc.unet_forward(sd_cpu, xc[done:done + 1]).numpy()[0]
-            ref = orc.masks_from_logits(lg)
-            ious += [orc.mask_iou(mk[done, i], ref[f]) for i, f in enumerate(orc.FIELDS)]
-            done += 1
-        t_cpu = time.perf_counter() - t0
-        cpu = {"value": round(done / t_cpu, 4), "unit": "images/s", "cores": nthreads, "kind": "port",
-               "sample": f"{done} of the bench images, batch 1, {S}x{S}, fp32 eager torch (oracle/unet_oracle.py)",
-               "iou_vs_cpu": {"min": round(min(ious), 5), "mean": round(float(np.mean(ious)), 5),
-                              "images": done, "gpu_dtype": args.dtype}}
+        cpu = cpu_baseline(args, model, x, masks, C, S)
+    lat = None
+    if rank == 0 and world == 1 and not args.no_latency and S == 512 and C == 3:
+        lat = gpu_latency(args, model, dev)
 
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16+fp16" if args.dtype == "mixed" else args.dtype,
             "data": f"synthetic (seeded invoice-like pages, gray x3; '{args.weights}' seeded weights -- "
                     "the trained checkpoint is an LFS pointer)",
             "config": {"workload": f"UNet(n_channels={C}, n_classes=3) forward {S}x{S} + fused sigmoid/"
                                    f"threshold bit-packed masks" + (" + RCCL all-gather" if world > 1 else ""),
                        "global_batch": world * B, "per_gpu_batch": B, "image": S,
-                       "parallelism": f"dp{world}"},
-            "roofline": roofline, "cpu_baseline": cpu, "step_ms": step_ms, "kernels": kernels, "layer_ms": layer_ms,
+                       "parallelism": f"dp{world}", "precision_plan": PLAN[args.dtype]},
+            "roofline": roofline, "cpu_baseline": cpu, "latency_bs1": lat, "step_ms": step_ms,
+            "kernels": kernels, "layer_ms": layer_ms,
         }
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

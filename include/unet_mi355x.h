@@ -14,9 +14,13 @@
  *     message for the calling thread.  C++ exceptions never cross the ABI.
  *   - device pointers are caller-owned (e.g. torch data_ptr()); work is enqueued on the
  *     caller's HIP stream (hipStream_t passed as void*), with no hidden synchronisation
- *     except inside unet_load_weights / unet_reserve (allocation + upload).
- *   - a handle is not re-entrant: it owns one workspace.  Use one handle per device and
- *     serialise calls on it (the Python wrapper does).
+ *     except inside unet_load_weights / unet_reserve (allocation + upload) and the first
+ *     unet_preprocess of a new photo geometry (coefficient upload).  unet_forward never
+ *     allocates: size the workspace with unet_reserve first.
+ *   - a handle owns one workspace.  Calls on it must not overlap on the host (serialise them;
+ *     the Python wrapper holds a lock).  On the device, a call issued on a different stream than
+ *     the previous one waits for that previous call (hipStreamWaitEvent), so the workspace is
+ *     never shared by two forwards in flight.
  */
 #ifndef UNET_MI355X_H
 #define UNET_MI355X_H
@@ -43,10 +47,15 @@ extern "C" {
 #define UNET_DTYPE_F32 0
 #define UNET_DTYPE_BF16 1
 #define UNET_DTYPE_F16 2
+/* bf16 at resolution levels 2-4, fp16 at the two full-resolution levels 0-1 (where the mask
+ * boundaries are decided): the precision plan of the headline benchmark, see DESIGN.md §4 */
+#define UNET_DTYPE_MIXED 3
 
 /* input layouts / dtypes accepted by unet_forward */
-#define UNET_LAYOUT_NCHW 0
-#define UNET_IN_F32 0
+#define UNET_LAYOUT_NCHW 0   /* [N][n_channels][H][W] (the reference's torch layout)             */
+#define UNET_LAYOUT_NHWC 1   /* [N][H][W][n_channels] (decoded photos)                           */
+#define UNET_IN_F32 0        /* float32 values                                                   */
+#define UNET_IN_U8 1         /* uint8 values v, read as v / 255.0f (inference.py:40's scaling)   */
 
 /* mask outputs of unet_forward */
 #define UNET_MASK_NONE 0
@@ -83,11 +92,14 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* tensors, int n);
 /* Bytes of device workspace unet_forward needs for (N, H, W). */
 size_t unet_workspace_bytes(const unet_handle* h, int N, int H, int W);
 
-/* Allocate (grow) the workspace for up to (N, H, W) so that later unet_forward calls
- * neither allocate nor synchronise (graph-capturable). */
+/* Allocate (grow) the workspace for up to (N, H, W): unet_forward requires it (UNET_ESTATE
+ * otherwise) and then neither allocates nor synchronises (graph-capturable).  Growing waits for
+ * the handle's queued work. */
 int unet_reserve(unet_handle* h, int N, int H, int W);
 
-/* Forward pass.  x: device fp32 NCHW [N][n_channels][H][W].
+/* Forward pass.  x: device tensor [N][n_channels][H][W] (x_layout UNET_LAYOUT_NCHW) or
+ * [N][H][W][n_channels] (UNET_LAYOUT_NHWC) of fp32 (x_dtype UNET_IN_F32) or uint8 (UNET_IN_U8,
+ * value / 255).
  * logits: device fp32 NCHW [N][n_classes][H][W] or NULL.
  * masks:  device uint8 per mask_kind or NULL (mask_kind UNET_MASK_NONE).
  * H, W must be divisible by 16 (the reference raises inside torch.cat otherwise).
@@ -146,6 +158,19 @@ int unet_forward_timed(unet_handle* h, const void* x, int x_layout, int x_dtype,
  * dst: device buffer receiving fp32 NCHW [N][C][h][w]; *numel receives the element count
  * when dst is NULL. */
 int unet_debug_fetch(unet_handle* h, const char* name, float* dst, size_t* numel, void* hip_stream);
+
+/* hipGraph of one forward (unet_forward, or unet_forward_boxes when boxes != NULL) over fixed
+ * device buffers and a fixed (N, H, W): the 22-launch sequence is captured once and replayed by
+ * unet_graph_launch with one host call -- the launch-bound small-batch case (run_unet's batch
+ * of 1, inference.py:42).  A graph is stale (UNET_ESTATE at launch) once unet_load_weights or a
+ * growing unet_reserve re-allocates the handle's device memory; capture again then.  Destroy
+ * graphs before their handle. */
+typedef struct unet_graph unet_graph;
+int unet_graph_create(unet_handle* h, const void* x, int x_layout, int x_dtype,
+                      void* logits, void* masks, int mask_kind, int32_t* boxes,
+                      int N, int H, int W, unet_graph** out);
+int unet_graph_launch(unet_graph* g, void* hip_stream);
+int unet_graph_destroy(unet_graph* g);
 
 int unet_destroy(unet_handle* h);
 

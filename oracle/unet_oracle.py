@@ -114,3 +114,45 @@ def mask_iou(a: np.ndarray, b: np.ndarray) -> float:
     if union == 0:
         return 1.0
     return float(np.logical_and(a, b).sum() / union)
+
+
+# ---- run_unet restated on the CPU (inference.py:17-129): the CPU baseline's end-to-end leg ----
+
+def load_model_state(checkpoint_path: str):
+    """inference.py:17-24 on the CPU: build the UNet(3, 3) module tree (parameter allocation and
+    default init, as ``UNet(3, 3)`` does), torch.load the checkpoint, strict load_state_dict,
+    eval; returns the loaded state_dict the functional forward reads."""
+    from unet_mi355x.model import UNet as _ModuleTree   # the reference's module tree, parameters only
+    model = _ModuleTree(3, 3)
+    state = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+    model.load_state_dict(state)
+    model.eval()
+    return {k: v.detach() for k, v in model.state_dict().items()}
+
+
+def preprocess(pil_img) -> torch.Tensor:
+    """inference.py:30-44: RGB, /255 in float32, HWC -> CHW, batch of 1."""
+    arr = np.array(pil_img.convert("RGB")).astype(np.float32) / 255.0
+    if arr.ndim != 3 or arr.shape[2] != 3:
+        raise ValueError(f"Invalid image shape: {arr.shape}")
+    return torch.from_numpy(arr.transpose(2, 0, 1)).unsqueeze(0)
+
+
+def run_unet(pil_img, checkpoint_path: str):
+    """inference.py:50-129: load the model (every call, :58), resize to 512 with PIL's default
+    filter (:63), forward, sigmoid + thresholds (:72-79), bbox -> 15 % pad -> crop, rejecting
+    empty / degenerate / near-black crops (:84-127).  Returns (masks, crops)."""
+    sd = load_model_state(checkpoint_path)
+    ow, oh = pil_img.size
+    x = preprocess(pil_img.resize((IMG_SIZE, IMG_SIZE)))
+    logits = unet_forward(sd, x).numpy()[0]
+    masks = masks_from_logits(logits)
+    crops = {}
+    for key, box in crop_boxes(masks, ow, oh).items():
+        crop = None if box is None else pil_img.crop(box)
+        if crop is not None:
+            arr = np.array(crop)
+            if arr.size == 0 or arr.mean() < 3:
+                crop = None
+        crops[key] = crop
+    return masks, crops

@@ -1,6 +1,8 @@
 """Multi-rank batch sharding + mask all-gather with the gloo backend on CPU,
-world_size 2 and 3.  The per-rank 'segmenter' is a deterministic stand-in (no GPU here);
-the GPU path runs the same ShardedSegmenter with the native forward (bench.py, N>1)."""
+world_size 2 and 3.  The collective is the same call the bench's RCCL path makes
+(all_gather_into_tensor; gloo implements it on CPU), and the bench's N>1 step and timing loop
+(unet_mi355x.dist.sharded_mask_step / timed_steps, used verbatim by bench.py) run here with a
+deterministic CPU stand-in for the per-rank forward (no GPU here)."""
 import os
 import socket
 
@@ -9,7 +11,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from unet_mi355x.dist import ShardedSegmenter, all_gather_rows, shard_bounds
+import time
+
+from unet_mi355x.dist import ShardedSegmenter, all_gather_rows, shard_bounds, sharded_mask_step, timed_steps
 
 
 def _free_port():
@@ -75,3 +79,49 @@ def test_shard_bounds_cover_batch():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
             assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def _bench_worker(rank, world, port, per_rank, q):
+    """bench.py's N>1 step: each rank holds its own per-GPU batch (weak scaling), forwards it
+    into its bit-packed mask buffer and all-gathers; timing = max over ranks."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        x_global = torch.randn(world * per_rank, 3, 16, 16)
+        x_local = x_global[rank * per_rank:(rank + 1) * per_rank].contiguous()
+        masks_local = torch.empty((per_rank, 3, 4, 8), dtype=torch.uint8)
+        calls = []
+
+        def segment(xl, ml):       # stand-in for handle.forward(x, None, masks, MASK_BITS, stream)
+            ml.copy_(fake_masks(xl))
+            calls.append(xl.shape[0])
+
+        gathered = []
+
+        def step():
+            time.sleep(0.02 * (rank + 1))        # ranks finish at different times
+            gathered.append(sharded_mask_step(segment, x_local, masks_local, world * per_rank))
+
+        elapsed, per_step = timed_steps(step, steps=3, warmup=1)
+        ok = all(torch.equal(g, fake_masks(x_global)) for g in gathered) and len(gathered) == 4
+        # the reported time is the slowest rank's: >= 3 steps of the last rank's 0.02*world s
+        q.put((rank, ok, elapsed >= 3 * 0.02 * world, len(per_step) == 3 and calls == [per_rank] * 4))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,per_rank", [(2, 4), (3, 2)])
+def test_bench_step_and_timing_under_gloo(world, per_rank):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, per_rank, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(r[0] for r in res) == list(range(world))
+    assert all(all(r[1:]) for r in res), res

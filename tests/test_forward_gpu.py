@@ -1,14 +1,17 @@
 """Parity of the native MI355X forward (through the C-ABI) against the golden vectors the
 reference produced and against the CPU oracle.  Needs a GPU: run with -m gpu.
 
-Tolerances (max |err| / max(1, max|ref|)):
-  fp32 path (exact-fp32 MFMA, different summation order)  <= 1e-4
-  fp16 path (fp16 storage, fp32 accumulate)                <= 1.5e-2
-  bf16 path (bf16 storage, fp32 accumulate)                <= 8e-2
-Masks (fp32 path) must match the oracle to IoU >= 0.999 (north_star); 16-bit IoUs are
-reported and bounded below.
+Logit tolerances, max |err| / max(1, max|ref|) (TOL; measured on MI355X in round 2, see
+profiles/gpu_tests_r2*.log, and set at about 2x the largest value measured over the goldens):
+  fp32  (exact-fp32 MFMA, different summation order)             measured <= 5e-6
+  fp16  (fp16 storage, fp32 accumulate)                          measured <= 2.2e-3
+  bf16  (bf16 storage, fp32 accumulate)                          measured <= 1.7e-2
+  mixed (bf16 at levels 2-4, fp16 at levels 0-1: the bench plan)
+Masks: fp32 must match the oracle to IoU >= 0.999 (north_star); on trained-like weights the
+bench plan ("mixed") and fp16 meet 0.999 too, pure bf16 does not (0.998).
 """
 import glob
+import hashlib
 import os
 import tempfile
 
@@ -17,13 +20,15 @@ import pytest
 import torch
 
 from oracle import unet_oracle as orc
+from unet_mi355x import native
 from unet_mi355x import synthetic as syn
 from unet_mi355x.model import UNet
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-TOL = {"fp32": 1e-4, "fp16": 1.5e-2, "bf16": 8e-2}
+TOL = {"fp32": 1e-4, "fp16": 5e-3, "bf16": 3.5e-2, "mixed": 3.5e-2}
 DEV = "cuda:0"
+HALO_CFGS, RING_CFGS, UP_CFGS = [0, 1, 2], [3, 4, 5], [2, 6, 7]   # csrc/unet_internal.h Cfg
 
 
 def make_model(sd_np, c, dtype):
@@ -36,7 +41,7 @@ def rel_err(out, ref):
     return float(np.abs(out - ref).max()) / max(1.0, float(np.abs(ref).max()))
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16", "mixed"])
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "unet_*.npz"))), ids=os.path.basename)
 def test_golden_logits(path, dtype):
     z = np.load(path)
@@ -53,7 +58,7 @@ def test_golden_logits(path, dtype):
     m.close()
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "mixed"])
 def test_golden_intermediates(dtype):
     """Per-layer localisation: skips, pools, bottleneck and up-convs vs the reference hooks."""
     z = np.load(os.path.join(GOLD, "unet_c3_h16w16_n3_structured.npz"))
@@ -70,6 +75,44 @@ def test_golden_intermediates(dtype):
         err = rel_err(got, ref)
         print(f"{name} {dtype}: rel err {err:.3e}")
         assert err <= TOL[dtype], name
+    m.close()
+
+
+def _golden_photo_input(m):
+    """The 600x400 golden photo through the device preprocessing (inference.py:62-64)."""
+    from PIL import Image
+    z = np.load(os.path.join(GOLD, "run_unet_600x400.npz"))
+    img = torch.from_numpy(np.ascontiguousarray(np.asarray(Image.fromarray(z["image"], mode="RGB")))).to(DEV)
+    return z, m.preprocess(img, 512)
+
+
+def test_preprocess_equals_reference_input_bitwise():
+    """unet_preprocess of the golden photo is the reference's own network input, byte for byte
+    (sha256 of inference.preprocess(pil.resize((512, 512))), make_golden.py)."""
+    m = make_model(syn.make_state_dict(0, 3, 3), 3, "bf16")
+    z, x = _golden_photo_input(m)
+    xh = x.cpu().numpy()
+    assert xh.shape == (1, 3, 512, 512) and xh.dtype == np.float32
+    assert hashlib.sha256(xh.tobytes()).hexdigest() == str(z["x_sha256"])
+    assert np.array_equal(xh[0, :, ::8, ::8], z["x_sub8"])
+    m.close()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16", "mixed"])
+def test_reference_512_logits(dtype):
+    """Full-size (512x512) logits pinned to the REFERENCE's own forward on its run_unet input:
+    the stored 1/4-subsampled grid and rows 0 and 257 (make_golden.py, inference.py:62-67)."""
+    z = np.load(os.path.join(GOLD, "run_unet_600x400.npz"))
+    sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile="structured")
+    sd["out_conv.bias"] = sd["out_conv.bias"] + z["out_bias_delta"]
+    m = make_model(sd, 3, dtype)
+    _, x = _golden_photo_input(m)
+    with torch.no_grad():
+        lg = m(x).cpu().numpy()[0]
+    errs = {"sub4": rel_err(lg[:, ::4, ::4], z["logits_sub4"]), "row0": rel_err(lg[:, 0, :], z["logits_row0"]),
+            "row257": rel_err(lg[:, 257, :], z["logits_row257"])}
+    print(f"512x512 reference logits {dtype}: " + ", ".join(f"{k} {v:.3e}" for k, v in errs.items()))
+    assert max(errs.values()) <= TOL[dtype]
     m.close()
 
 
@@ -98,12 +141,15 @@ def _recentred(seed, x, c=3):
 
 
 def test_masks_512_all_dtypes():
-    """Full-size 512x512 pages: fused masks (u8 and bit-packed) vs the oracle's masks."""
+    """Full-size 512x512 pages, untrained (structured) weights: logits within tolerance of the
+    oracle, fused masks (u8 and bit-packed agree) vs the oracle's masks.  Untrained weights put
+    ~20 % of the pixels near a threshold, so the 16-bit IoU bounds here are loose; the
+    trained-like case is test_masks_512_pretrained_weights."""
     x = syn.invoice_pages(21, 2, 512, 512, 3)
     sd, ref_logits = _recentred(21, x)
     ref_masks = np.stack([np.stack(list(orc.masks_from_logits(ref_logits[i]).values())) for i in range(2)])
     xd = torch.from_numpy(x).to(DEV)
-    for dtype, min_iou in (("fp32", 0.999), ("fp16", 0.99), ("bf16", 0.95)):
+    for dtype, min_iou in (("fp32", 0.999), ("fp16", 0.99), ("mixed", 0.97), ("bf16", 0.95)):
         m = make_model(sd, 3, dtype)
         with torch.no_grad():
             masks, logits = m.forward_masks(xd, with_logits=True)
@@ -111,9 +157,10 @@ def test_masks_512_all_dtypes():
         masks = masks.cpu().numpy().astype(bool)
         unpacked = np.unpackbits(bits.cpu().numpy(), axis=-1, bitorder="little").astype(bool)
         assert np.array_equal(unpacked, masks), "bit-packed and u8 masks disagree"
+        err = rel_err(logits.cpu().numpy(), ref_logits)
         ious = [orc.mask_iou(masks[i, k], ref_masks[i, k]) for i in range(2) for k in range(3)]
-        print(f"512x512 {dtype}: logits rel err {rel_err(logits.cpu().numpy(), ref_logits):.3e}, "
-              f"mask IoU min {min(ious):.5f} mean {np.mean(ious):.5f}")
+        print(f"512x512 {dtype}: logits rel err {err:.3e}, mask IoU min {min(ious):.5f} mean {np.mean(ious):.5f}")
+        assert err <= TOL[dtype]
         assert min(ious) >= min_iou
         m.close()
 
@@ -121,14 +168,14 @@ def test_masks_512_all_dtypes():
 def test_masks_512_pretrained_weights():
     """Trained-like weights (synthetic profile "pretrained": bimodal logits, as a trained net
     has): fused masks of every dtype vs the fp32 CPU oracle at 512x512 (north_star IoU
-    target 0.999)."""
+    target 0.999, met by fp32, fp16 and the bench's mixed plan)."""
     x = syn.invoice_pages(1000, 2, 512, 512, 3)
     sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
     ref_logits = orc.unet_forward(sd, torch.from_numpy(x)).numpy()
     ref_masks = np.stack([np.stack(list(orc.masks_from_logits(ref_logits[i]).values())) for i in range(2)])
     assert 0.02 < ref_masks.mean() < 0.5
     xd = torch.from_numpy(x).to(DEV)
-    for dtype, min_iou in (("fp32", 0.9999), ("fp16", 0.999), ("bf16", 0.99)):
+    for dtype, min_iou in (("fp32", 0.9999), ("fp16", 0.999), ("mixed", 0.999), ("bf16", 0.995)):
         m = make_model(sd, 3, dtype)
         with torch.no_grad():
             bits = m.forward_masks(xd, packed=True)
@@ -139,33 +186,167 @@ def test_masks_512_pretrained_weights():
         m.close()
 
 
-def test_run_unet_boundary_matches_reference_golden():
-    """inference.run_unet (drop-in) on the golden 600x400 photo vs the reference's masks/crops."""
-    from PIL import Image
-    import hashlib
-    from unet_mi355x import inference as inf
-    z = np.load(os.path.join(GOLD, "run_unet_600x400.npz"))
-    sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile="structured")
-    sd["out_conv.bias"] = sd["out_conv.bias"] + z["out_bias_delta"]
-    assert syn.state_dict_checksum(sd) == str(z["sd_sha256"])
-    pil = Image.fromarray(z["image"], mode="RGB")
-    with tempfile.TemporaryDirectory() as td:
-        ck = os.path.join(td, "best_unet_model.pth")
-        torch.save({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, ck)
-        inf.DEVICE = DEV
-        masks, crops = inf.run_unet(pil, ck, compute_dtype="fp32")
-    for k in inf.FIELDS:
-        ref = np.unpackbits(z["maskbits_" + k], axis=-1, bitorder="little").astype(bool)
-        iou = orc.mask_iou(masks[k], ref)
-        print(f"run_unet {k}: IoU {iou:.6f}, differing pixels {int((masks[k] != ref).sum())}")
-        assert iou >= 0.999
-        if bool(z["crop_none_" + k]):
-            assert crops[k] is None
-        else:
-            arr = np.asarray(crops[k])
-            assert list(arr.shape) == list(z["crop_shape_" + k])
-            if np.array_equal(masks[k], ref):
-                assert hashlib.sha256(arr.tobytes()).hexdigest() == str(z["crop_sha256_" + k])
+def test_batch256_bench_shape_invariance_and_iou():
+    """The batch the bench times (256 pages of 512x512, the bench's mixed plan, bit-packed
+    masks): image i of the N=256 forward equals the same image run alone (N=1) and in the
+    second half-batch (N=128, rank 1's shard of a 2-GPU run) bit for bit -- the persistent
+    walkers wrap ~100x more often at N=256 than in the small tests --, and the masks of 4
+    sampled pages match the fp32 oracle at IoU >= 0.999."""
+    import bench
+    sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
+    m = make_model(sd, 3, "mixed")
+    x = torch.from_numpy(bench.gen_pages(1000, 256, 512, 3, unique=64)).to(DEV)
+    with torch.no_grad():
+        full = m.forward_masks(x, packed=True).clone()
+        half = m.forward_masks(x[128:].contiguous(), packed=True)
+    assert torch.equal(half, full[128:]), "N=128 shard differs from the N=256 batch"
+    sample = [0, 77, 128, 255]
+    ious = []
+    for i in sample:
+        with torch.no_grad():
+            one = m.forward_masks(x[i:i + 1].contiguous(), packed=True)
+        assert torch.equal(one, full[i:i + 1]), f"image {i}: N=1 differs from N=256"
+        ref = orc.masks_from_logits(orc.unet_forward(sd, x[i:i + 1].cpu()).numpy()[0])
+        got = np.unpackbits(full[i].cpu().numpy(), axis=-1, bitorder="little").astype(bool)
+        ious += [orc.mask_iou(got[k], ref[f]) for k, f in enumerate(orc.FIELDS)]
+    print(f"bs256 mixed: IoU vs oracle min {min(ious):.5f} mean {np.mean(ious):.5f}")
+    assert min(ious) >= 0.999
+    m.close()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "mixed"])
+def test_nan_input_propagates_like_torch(dtype):
+    """A NaN input pixel propagates exactly as through the reference's aten ops: conv spreads it
+    over the 3x3 neighbourhood, ReLU and MaxPool2d keep it (unet_model.py:12,16,34), so the NaN
+    logits form the same receptive-field pattern as the oracle's; the other logits stay within
+    tolerance and a NaN logit gives a False mask (sigmoid(NaN) > thr is False)."""
+    sd = syn.make_state_dict(3, 3, 3, profile="structured")
+    x = syn.uniform_batch(8, 1, 3, 320, 320)
+    x[0, 1, 7, 9] = np.nan
+    x[0, 0, 300, 170] = np.nan
+    ref = orc.unet_forward(sd, torch.from_numpy(x)).numpy()
+    m = make_model(sd, 3, dtype)
+    with torch.no_grad():
+        masks, lg = m.forward_masks(torch.from_numpy(x).to(DEV), with_logits=True)
+    lg, masks = lg.cpu().numpy(), masks.cpu().numpy()
+    nan_ref, nan_got = np.isnan(ref), np.isnan(lg)
+    print(f"{dtype}: NaN logits {int(nan_got.sum())} (oracle {int(nan_ref.sum())}) of {lg.size}")
+    assert 0 < nan_ref.sum() < ref.size
+    assert np.array_equal(nan_got, nan_ref)
+    ok = ~nan_ref
+    assert rel_err(lg[ok], ref[ok]) <= TOL[dtype]
+    assert not masks[nan_got].any()
+    m.close()
+
+
+def test_logit_cut_matches_torch_sigmoid_on_gpu():
+    """The fused masks threshold logits at the host-bisected cut (unet_logit_cut); the reference
+    thresholds torch.sigmoid.  Against ROCm's own sigmoid on the GPU, every fp32 logit within
+    4096 ulps of each field's cut classifies the same way, except at most a hair from the cut
+    (the ulp-level disagreement of two fp32 sigmoid implementations)."""
+    lib = native.load_library()
+    for thr in (0.25, 0.40, 0.30):
+        cut = np.float32(lib.unet_logit_cut(thr))
+        bits = cut.view(np.int32).astype(np.int64) + np.arange(-4096, 4097)
+        x = torch.from_numpy(bits.astype(np.int32).view(np.float32)).to(DEV)
+        theirs = (torch.sigmoid(x) > thr).cpu().numpy()
+        ours = (x > float(cut)).cpu().numpy()
+        diff = np.nonzero(ours != theirs)[0] - 4096
+        print(f"thr {thr}: cut {float(cut)!r}, ulps that disagree with torch.sigmoid on the GPU: {diff.tolist()}")
+        assert np.all(np.abs(diff) <= 2)
+
+
+def test_two_streams_share_one_handle():
+    """forwards issued on two torch streams against ONE handle (one workspace) give
+    bitwise the results of the same forwards issued back to back on one stream -- the library
+    orders a call after the previous call on another stream (hipStreamWaitEvent)."""
+    sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
+    m = make_model(sd, 3, "mixed")
+    xa = torch.from_numpy(syn.invoice_pages(31, 8, 512, 512, 3)).to(DEV)
+    xb = torch.from_numpy(syn.invoice_pages(32, 8, 512, 512, 3)).to(DEV)
+    with torch.no_grad():
+        ra = m.forward_masks(xa, packed=True).clone()
+        rb = m.forward_masks(xb, packed=True).clone()
+        sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+        sa.wait_stream(torch.cuda.current_stream())
+        sb.wait_stream(torch.cuda.current_stream())
+        outs = []
+        for _ in range(3):
+            with torch.cuda.stream(sa):
+                a = m.forward_masks(xa, packed=True)
+            with torch.cuda.stream(sb):
+                b = m.forward_masks(xb, packed=True)
+            outs.append((a, b))
+        torch.cuda.synchronize()
+    for a, b in outs:
+        assert torch.equal(a, ra) and torch.equal(b, rb)
+    m.close()
+
+
+def test_graph_replay_equals_eager():
+    """unet_graph_create / unet_graph_launch (the hipGraph-captured forward, batch 1 and 4)
+    produce bitwise the eager forward's logits, masks and boxes; a weight reload makes the graph
+    stale (UNET_ESTATE) instead of replaying freed pointers."""
+    sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
+    m = make_model(sd, 3, "mixed")
+    h = m.native_handle(torch.device(DEV))
+    stream = torch.cuda.current_stream().cuda_stream
+    for n in (1, 4):
+        x = torch.from_numpy(syn.invoice_pages(40 + n, n, 512, 512, 3)).to(DEV)
+        lg = torch.empty((n, 3, 512, 512), device=DEV)
+        mk = torch.empty((n, 3, 512, 64), dtype=torch.uint8, device=DEV)
+        bx = torch.empty((n, 3, 4), dtype=torch.int32, device=DEV)
+        h.reserve(n, 512, 512)
+        h.forward_boxes(x, lg, mk, native.MASK_BITS, bx, stream)
+        ref = (lg.clone(), mk.clone(), bx.clone())
+        g = h.graph(x, lg, mk, native.MASK_BITS, boxes=bx)
+        for t in (lg, mk, bx):
+            t.zero_()
+        for _ in range(3):
+            g.launch(stream)
+        torch.cuda.synchronize()
+        assert torch.equal(lg, ref[0]) and torch.equal(mk, ref[1]) and torch.equal(bx, ref[2])
+    h.load_weights(m.state_dict())
+    with pytest.raises(RuntimeError, match="stale"):
+        g.launch(stream)
+    g.close()
+    m.close()
+
+
+def test_u8_nhwc_input_equals_f32_nchw():
+    """unet_forward's other input formats (include/unet_mi355x.h): uint8 NHWC photos (value/255)
+    give bitwise the result of the same values as fp32 NCHW, on the 16-bit and the fp32 path."""
+    rng = np.random.default_rng(5)
+    u8 = rng.integers(0, 256, (2, 128, 96, 3), dtype=np.uint8)
+    f32 = np.ascontiguousarray((u8.astype(np.float32) / np.float32(255.0)).transpose(0, 3, 1, 2))
+    sd = syn.make_state_dict(0, 3, 3, profile="structured")
+    for dtype in ("mixed", "fp32"):
+        m = make_model(sd, 3, dtype)
+        h = m.native_handle(torch.device(DEV))
+        stream = torch.cuda.current_stream().cuda_stream
+        h.reserve(2, 128, 96)
+        outs = []
+        for x, layout in ((torch.from_numpy(f32).to(DEV), native.LAYOUT_NCHW),
+                          (torch.from_numpy(u8).to(DEV), native.LAYOUT_NHWC),
+                          (torch.from_numpy(f32.transpose(0, 2, 3, 1).copy()).to(DEV), native.LAYOUT_NHWC)):
+            lg = torch.empty((2, 3, 128, 96), device=DEV)
+            h.forward(x, lg, None, native.MASK_NONE, stream, layout=layout)
+            outs.append(lg)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), dtype
+        m.close()
+
+
+def test_bf16_cast_model_loads():
+    """a UNet cast with .to(torch.bfloat16) still loads (its parameters are read back
+    in fp32, as the reference module's would be) and gives the fp32-weights result of that cast."""
+    sd = syn.make_state_dict(0, 3, 3, profile="structured")
+    m = make_model(sd, 3, "bf16").to(torch.bfloat16)
+    x = torch.from_numpy(syn.uniform_batch(1, 1, 3, 32, 32)).to(DEV)
+    with torch.no_grad():
+        out = m(x)
+    assert out.dtype == torch.float32 and torch.isfinite(out).all()
+    m.close()
 
 
 def test_errors_and_no_fallback():
@@ -176,6 +357,11 @@ def test_errors_and_no_fallback():
         m(torch.zeros(1, 3, 32, 32))
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 1, 32, 32, device=DEV))
+    h = m.native_handle(torch.device(DEV))   # forwards never allocate: an unreserved shape is refused
+    x = torch.zeros(64, 3, 512, 512, device=DEV)
+    with pytest.raises(RuntimeError, match="unet_reserve"):
+        h.forward(x, None, torch.empty((64, 3, 512, 64), dtype=torch.uint8, device=DEV), native.MASK_BITS,
+                  torch.cuda.current_stream().cuda_stream)
     m.close()
 
 
@@ -191,10 +377,10 @@ def test_weight_update_repacks():
     m.close()
 
 
-@pytest.mark.parametrize("cfg", list(range(34)))
+@pytest.mark.parametrize("cfg", HALO_CFGS + RING_CFGS)
 def test_every_kernel_config(cfg, monkeypatch):
-    """Each implicit-GEMM configuration (csrc/unet_internal.h Cfg) forced on every 3x3 layer
-    it supports, checked against the reference golden (fp32 and bf16)."""
+    """Each 3x3 configuration (csrc/unet_internal.h Cfg) forced on every layer it supports,
+    checked against the reference golden (fp32 and bf16)."""
     monkeypatch.setenv("UNET_MI355X_CFG", ",".join(f"{i}:{cfg}" for i in range(17)))
     z = np.load(os.path.join(GOLD, "unet_c3_h64w64_n2_structured.npz"))
     sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile=str(z["profile"]))
@@ -208,7 +394,7 @@ def test_every_kernel_config(cfg, monkeypatch):
         m.close()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 4, 5, 8, 9, 14, 15, 21, 22, 32, 34, 35, 36])
+@pytest.mark.parametrize("cfg", UP_CFGS)
 def test_convtranspose_configs(cfg, monkeypatch):
     """ConvTranspose2d (up4..up1) on every supported kernel configuration vs the golden."""
     monkeypatch.setenv("UNET_MI355X_UPCFG", ",".join(f"{i}:{cfg}" for i in range(4)))
@@ -251,15 +437,15 @@ def _forced(cfg, up, sd, x, dtype, monkeypatch):
     return st
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp32", "mixed"])
 def test_forward_deterministic_and_config_invariant(dtype, monkeypatch):
     """Full-size pages (persistent kernels walk several tiles per block, rings wrap): repeated
     forwards are bitwise identical, and within each kernel family every configuration --
     forced on all 3x3 layers, or on all ConvTranspose layers -- gives bitwise the same
-    activations: the 128-byte LDS-halo configurations 4..26 (K order chunk64-major /
-    tap-minor) agree with each other, the 64-byte ring configurations 27..31 and 33 (chunk32-major; 33 = down1.0 fused)
-    agree with each other, and the ConvTranspose configurations agree with the defaults.  A
-    missed wait in a DMA ring shows up here as a run-to-run or config-to-config difference."""
+    activations: the 128-byte LDS-halo configurations (K order chunk64-major / tap-minor) agree
+    with each other, the 64-byte ring configurations (chunk32-major; 5 = down1.0 fused) agree
+    with each other, and the ConvTranspose configurations agree with the defaults.  A missed
+    wait in a DMA ring shows up here as a run-to-run or config-to-config difference."""
     x = torch.from_numpy(syn.invoice_pages(3, 2, 512, 512, 3)).to(DEV)
     sd = syn.make_state_dict(3, 3, 3, profile="structured")
     m = make_model(sd, 3, dtype)
@@ -267,14 +453,16 @@ def test_forward_deterministic_and_config_invariant(dtype, monkeypatch):
     for r in range(2):
         assert _first_diff(_forward_state(m, x), base) == [], f"run {r + 1} differs"
     m.close()
+    if dtype == "mixed":
+        return
     bad = []
-    for family in (list(range(4, 27)), list(range(27, 32)) + [33]):
+    for family in (HALO_CFGS, RING_CFGS):
         fbase = _forced(family[0], None, sd, x, dtype, monkeypatch)
         for cfg in family[1:]:
             d = _first_diff(_forced(cfg, None, sd, x, dtype, monkeypatch), fbase)
             if d:
                 bad.append((cfg, None, d[:3]))
-    for up in (4, 5, 8, 9, 14, 15, 21, 22, 23, 25, 32, 34, 35, 36):
+    for up in UP_CFGS:
         d = _first_diff(_forced(None, up, sd, x, dtype, monkeypatch), base)
         if d:
             bad.append((None, up, d[:3]))
@@ -302,7 +490,7 @@ def test_mask_boxes_match_numpy(kind):
              (syn.make_state_dict(1, 3, 3, "torch_default"), syn.invoice_pages(2, 1, 64, 64, 3)),
              (syn.make_state_dict(5, 3, 3, "structured", out_bias=0.0), syn.uniform_batch(3, 3, 3, 32, 48))]
     for sd, x in cases:
-        m = make_model(sd, 3, "bf16")
+        m = make_model(sd, 3, "mixed")
         xd = torch.from_numpy(x).to(DEV)
         with torch.no_grad():
             ref_masks = m.forward_masks(xd).cpu().numpy().astype(bool)
@@ -365,6 +553,50 @@ def test_preprocess_bit_exact_with_pillow(h, w, c):
     m.close()
 
 
+def test_preprocess_geometry_cache_is_bounded():
+    """the per-geometry resize tables live in a bounded LRU; 20 distinct photo sizes
+    (more than the cache holds) still resize bit-exactly, including a geometry revisited after
+    its eviction."""
+    from PIL import Image
+    m = make_model(syn.make_state_dict(0, 3, 3), 3, "bf16")
+    rng = np.random.default_rng(2)
+    sizes = [(100 + 7 * i, 120 + 5 * i) for i in range(20)] + [(100, 120)]
+    for h, w in sizes:
+        arr = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        ref = np.array(Image.fromarray(arr).resize((512, 512))).astype(np.float32) / 255.0
+        got = m.preprocess(torch.from_numpy(arr).to(DEV)).cpu().numpy()[0]
+        assert np.array_equal(got, ref.transpose(2, 0, 1)), (h, w)
+    m.close()
+
+
+def test_run_unet_boundary_matches_reference_golden():
+    """inference.run_unet (drop-in) on the golden 600x400 photo vs the reference's masks/crops."""
+    from PIL import Image
+    from unet_mi355x import inference as inf
+    z = np.load(os.path.join(GOLD, "run_unet_600x400.npz"))
+    sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile="structured")
+    sd["out_conv.bias"] = sd["out_conv.bias"] + z["out_bias_delta"]
+    assert syn.state_dict_checksum(sd) == str(z["sd_sha256"])
+    pil = Image.fromarray(z["image"], mode="RGB")
+    with tempfile.TemporaryDirectory() as td:
+        ck = os.path.join(td, "best_unet_model.pth")
+        torch.save({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, ck)
+        inf.DEVICE = DEV
+        masks, crops = inf.run_unet(pil, ck, compute_dtype="fp32")
+    for k in inf.FIELDS:
+        ref = np.unpackbits(z["maskbits_" + k], axis=-1, bitorder="little").astype(bool)
+        iou = orc.mask_iou(masks[k], ref)
+        print(f"run_unet {k}: IoU {iou:.6f}, differing pixels {int((masks[k] != ref).sum())}")
+        assert iou >= 0.999
+        if bool(z["crop_none_" + k]):
+            assert crops[k] is None
+        else:
+            arr = np.asarray(crops[k])
+            assert list(arr.shape) == list(z["crop_shape_" + k])
+            if np.array_equal(masks[k], ref):
+                assert hashlib.sha256(arr.tobytes()).hexdigest() == str(z["crop_sha256_" + k])
+
+
 def test_run_unet_batch_equals_per_photo_calls():
     """inference.run_unet_batch (one forward over N photos of mixed sizes / modes) returns, for
     every photo, exactly run_unet's masks and crops."""
@@ -380,8 +612,8 @@ def test_run_unet_batch_equals_per_photo_calls():
         ck = os.path.join(td, "best_unet_model.pth")
         torch.save({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, ck)
         inf.DEVICE = DEV
-        single = [inf.run_unet(p, ck, compute_dtype="bf16") for p in photos]
-        batch = inf.run_unet_batch(photos, ck, compute_dtype="bf16")
+        single = [inf.run_unet(p, ck, compute_dtype="mixed") for p in photos]
+        batch = inf.run_unet_batch(photos, ck, compute_dtype="mixed")
     assert len(batch) == len(photos)
     for (m1, c1), (m2, c2) in zip(single, batch):
         for k in inf.FIELDS:

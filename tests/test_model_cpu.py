@@ -38,6 +38,15 @@ def test_forward_on_cpu_fails_loudly():
         m(torch.zeros(1, 3, 40, 32))
 
 
+def test_training_mode_raises_clearly():
+    """the drop-in is inference-only; training-mode use with grad enabled raises at the
+    call instead of returning eval-mode outputs without a graph (reference train.py imports UNet)."""
+    m = UNet(3, 3)
+    assert m.training
+    with pytest.raises(RuntimeError, match="inference-only"):
+        m(torch.zeros(1, 3, 32, 32))
+
+
 def test_bad_dtype_rejected():
     with pytest.raises(ValueError):
         UNet(3, 3, compute_dtype="int8")

@@ -69,3 +69,50 @@ def test_mask_threshold_semantics():
     m = orc.masks_from_logits(logits)
     assert m["invoice_no"][0, 0] and not m["invoice_no"][0, 1]
     assert orc.mask_iou(m["date"], m["date"]) == 1.0
+
+
+def test_oracle_matches_reference_512_logits():
+    """Full-size parity of the oracle with the reference: the reference's own run_unet input for
+    the golden 600x400 photo (PIL resize to 512 + inference.preprocess, pinned by its sha256) and
+    its 512x512 logits (1/4-subsampled grid, rows 0 and 257; make_golden.py)."""
+    from PIL import Image
+    z = np.load(os.path.join(GOLD, "run_unet_600x400.npz"))
+    sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile="structured")
+    sd["out_conv.bias"] = sd["out_conv.bias"] + z["out_bias_delta"]
+    assert syn.state_dict_checksum(sd) == str(z["sd_sha256"])
+    x = orc.preprocess(Image.fromarray(z["image"], mode="RGB").resize((512, 512)))
+    assert hashlib.sha256(x.numpy().tobytes()).hexdigest() == str(z["x_sha256"])
+    lg = orc.unet_forward(sd, x).numpy()[0]
+    for got, key in ((lg[:, ::4, ::4], "logits_sub4"), (lg[:, 0, :], "logits_row0"), (lg[:, 257, :], "logits_row257")):
+        ref = z[key]
+        np.testing.assert_allclose(got, ref, rtol=0, atol=2e-5 * max(1.0, float(np.abs(ref).max())), err_msg=key)
+    # and the masks / crops of the reference's run_unet follow from these logits
+    masks = orc.masks_from_logits(lg)
+    for k in orc.FIELDS:
+        ref = np.unpackbits(z["maskbits_" + k], axis=-1, bitorder="little").astype(bool)
+        assert orc.mask_iou(masks[k], ref) >= 0.9999, k
+
+
+def test_oracle_run_unet_matches_reference_golden():
+    """The CPU baseline's end-to-end leg (oracle.run_unet: checkpoint load, resize, forward,
+    masks, crops -- inference.py:50-129) reproduces the reference's run_unet golden."""
+    import tempfile
+    from PIL import Image
+    z = np.load(os.path.join(GOLD, "run_unet_600x400.npz"))
+    sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile="structured")
+    sd["out_conv.bias"] = sd["out_conv.bias"] + z["out_bias_delta"]
+    pil = Image.fromarray(z["image"], mode="RGB")
+    with tempfile.TemporaryDirectory() as td:
+        ck = os.path.join(td, "best_unet_model.pth")
+        torch.save({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, ck)
+        masks, crops = orc.run_unet(pil, ck)
+    for k in orc.FIELDS:
+        ref = np.unpackbits(z["maskbits_" + k], axis=-1, bitorder="little").astype(bool)
+        assert orc.mask_iou(masks[k], ref) >= 0.9999, k
+        if bool(z["crop_none_" + k]):
+            assert crops[k] is None
+        else:
+            arr = np.asarray(crops[k])
+            assert list(arr.shape) == list(z["crop_shape_" + k])
+            if np.array_equal(masks[k], ref):
+                assert hashlib.sha256(arr.tobytes()).hexdigest() == str(z["crop_sha256_" + k])

@@ -25,13 +25,18 @@ TYPES = {"f": "float", "DF16b": "__bf16", "DF16_": "_Float16"}
 
 
 def label_of(name):
-    """Our mangled kernel symbol -> "kernel<T, ints...>" (bench.py / unet_launch_label spelling)."""
-    m = re.match(r"_ZN4unet(\d+)(\w+?)I(DF16b|DF16_|f)((?:Li\d+E)+)E", name)
+    """Our mangled kernel symbol -> "kernel<args>" (bench.py / unet_launch_label spelling):
+    template arguments are element types (DF16b, DF16_, f) or ints (Li<n>E)."""
+    m = re.match(r"_ZN4unet(\d+)(\w+)", name)
     if not m:
         return name
-    kname = m.group(2)[:int(m.group(1))]
-    ints = re.findall(r"Li(\d+)E", m.group(4))
-    return f"{kname}<{TYPES[m.group(3)]}, {', '.join(ints)}>"
+    n = int(m.group(1))
+    kname, rest = m.group(2)[:n], m.group(2)[n:]
+    if not rest.startswith("I"):
+        return name
+    args = re.findall(r"DF16b|DF16_|Li-?\d+E|f(?=[DLfE])", rest[1:].split("EEv")[0] + "E")
+    toks = [TYPES[a] if a in TYPES else a[2:-1] for a in args]
+    return f"{kname}<{', '.join(toks)}>"
 
 
 def load_pass(d):
@@ -89,7 +94,7 @@ def main():
         wait = 100 * c.get("SQ_WAIT_ANY", 0) / max(1, c.get("SQ_WAVE_CYCLES", 0))
         algo = launch_bytes(e, a.batch, a.size, a.size, 3, a.esize)
         print(f"{e[0]:14s} {rd / 1e9:8.2f} {wr / 1e9:8.2f} {algo / 1e9:8.2f} {mfma_pct:10.1f} {conf:9.2f} {wait:9.1f}")
-        k = agg[labels.get(e[0]) or label_of(c.get("kernel_name", e[1]))]
+        k = agg[labels.get(e[0]) or label_of(c.get("kernel_name", e[0]))]
         k["launches"] += 1
         k["hbm_read_bytes"] += rd
         k["hbm_write_bytes"] += wr

@@ -1,9 +1,9 @@
 // C-ABI host layer of the MI355X UNet forward path (include/unet_mi355x.h).
 //
 // Owns: strict state_dict ingestion (unet_model.py:24-53 key set), eval-BatchNorm folding
-// (unet_model.py:11,15; eps 1e-5), weight pre-packing for the implicit-GEMM kernel, the
-// activation workspace, and the per-forward launch sequence that mirrors
-// UNet.forward (unet_model.py:55-86).
+// (unet_model.py:11,15; eps 1e-5), the per-layer storage-precision plan, weight pre-packing for
+// the implicit-GEMM kernels, the activation workspace, and the per-forward launch sequence that
+// mirrors UNet.forward (unet_model.py:55-86).
 #include "unet_internal.h"
 #include "../../include/unet_mi355x.h"
 
@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <list>
 #include <map>
 #include <string>
 #include <tuple>
@@ -68,12 +69,13 @@ inline int natural_of_packed(int rho) {
   return g + (r >> 2) * 16 + t * 4 + (r & 3);
 }
 
-bool is_fused_in(int cfg) { return cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8 || cfg == CFG_RING_FUSED_IN; }
-
 struct Layer {
-  int cin = 0, cout = 0, ctot = 0, taps = 9, cfg = CFG_R128_P128;
-  void* w = nullptr;   // packed [ctot][taps*cin] element type
-  float* b = nullptr;  // [ctot] natural order
+  int cin = 0, cout = 0, ctot = 0, taps = 9, cfg = CFG_RING_R128;
+  DType dt = DType::BF16;    // operand type (activations read + packed weights)
+  DType dto = DType::BF16;   // output type (type of the consumer's operand)
+  DType dtq = DType::BF16;   // pooled-map type (EPI_POOL layers)
+  void* w = nullptr;         // packed weights
+  float* b = nullptr;        // [ctot] natural order
 };
 
 // Device coefficient tables of one resize geometry (unet_preprocess), owned by the handle.
@@ -81,6 +83,7 @@ struct ResampleStore {
   ResamplePlan plan{};
   std::vector<void*> bufs;
 };
+constexpr size_t kResampleCacheMax = 16;   // geometries kept (LRU)
 
 struct Buffers {
   size_t tA, cat1, cat2, cat3, cat4, p1, p2, p3, p4, bnb, tB, mbits, xpx, total;  // byte offsets
@@ -90,9 +93,9 @@ struct Buffers {
 
 struct unet_handle {
   unet_config cfg{};
-  DType dt = DType::BF16;
+  DType dt = DType::BF16;   // storage element type of the workspace (bf16 / f16 plans: 2 bytes)
   float* w0 = nullptr;  // first conv folded fp32 [64][C][3][3]
-  void* w0p = nullptr;  // first conv packed [64][32] element type (16-bit MFMA path)
+  void* w0p = nullptr;  // first conv packed [64][32] (16-bit MFMA path, down1.3's operand type)
   void* w0r = nullptr;  // the same, rows ordered for the ring kernel's fused first conv:
                         // [cb][t][16][32], row (cb, t, r) = channel 32cb + 8(r>>2) + 4t + (r&3)
   float* b0 = nullptr;
@@ -106,11 +109,25 @@ struct unet_handle {
   size_t ws_bytes = 0;
   int lastN = 0, lastH = 0, lastW = 0;
   std::vector<void*> allocs;
-  std::map<std::tuple<int, int, int, int>, ResampleStore> resample;   // (ih, iw, oh, ow) -> tables
+  // (ih, iw, oh, ow) -> tables, most recently used first
+  std::list<std::pair<std::tuple<int, int, int, int>, ResampleStore>> resample;
   uint8_t* pp_tmp = nullptr;              // horizontal-pass rows of unet_preprocess
   size_t pp_tmp_bytes = 0;
   std::string labels[UNET_NUM_LAUNCHES];   // kernel instantiation of every launch
   float thr_logit[kMaxClasses];           // per-class logit cut, see unet_logit_cut
+  // stream ordering of the shared workspace: the last call's completion event and stream
+  hipEvent_t done = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool pending = false;
+  bool capturing = false;        // inside unet_graph_create: no event record / wait in the stream
+  unsigned long long generation = 1;   // bumped whenever device pointers a graph captured change
+};
+
+struct unet_graph {
+  unet_handle* h = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  unsigned long long generation = 0;
 };
 
 namespace {
@@ -125,24 +142,44 @@ const int kLayerCh[17][2] = {{64, 64},    {64, 128},   {128, 128}, {128, 256}, {
                              {256, 512},  {512, 512},  {512, 1024}, {1024, 1024},
                              {1024, 512}, {512, 512},  {512, 256}, {256, 256},
                              {256, 128},  {128, 128},  {128, 64},  {64, 64}};
-// Default kernel configuration per 3x3 layer, from in-process A/B timing on MI355X at
-// bs256 512x512 bf16 (tools/tune.py; profiles/tune_r1*.txt).  All are two-blocks-per-CU
-// single-halo tiles; 128-row x 64-pixel wave tiles (fewer LDS reads per MFMA) win on the
-// plain-store layers, 64x64 wave tiles on the deeper pooled layers and at 512x512.
-const int kDefaultCfg[17] = {
-    CFG_FUSED_IN_W8,                                             // down1.0 + down1.3 (+pool), fused
-    CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // down2.0, down2.3 (+pool)
-    CFG_HALO1_R128T8_NS2, CFG_HALO1_R64_W4,                      // down3.0, down3.3 (+pool)
-    CFG_HALO1_R128T8_NS2, CFG_HALO1_R64_W4,                      // down4.0, down4.3 (+pool)
-    CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // bottleneck.0 .3
-    CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // conv4.0 conv4.3
-    CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // conv3.0 conv3.3
-    CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,                  // conv2.0 conv2.3
-    CFG_HALO1_R64_W4, CFG_HALO1_R64_W8};                         // conv1.0, conv1.3 (+head)                     // conv1.0, conv1.3 (+head)
-const int kDefaultUpCfg[4] = {CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2, CFG_HALO1_R128T8_NS2,
-                               CFG_HALO1_R128T8_NS2};  // up4..up1
+// Resolution level (0 = full resolution) of each 3x3 layer's input and output; EPI_POOL layers
+// also write a pooled map one level down.  ConvTranspose up_k reads level k and writes k-1.
+const int kLayerLevel[17] = {0, 1, 1, 2, 2, 3, 3, 4, 4, 3, 3, 2, 2, 1, 1, 0, 0};
+const int kUpLevel[4] = {4, 3, 2, 1};   // input level of up4..up1
+// Default kernel configuration per 3x3 layer, from in-process A/B timing on MI355X at bs256
+// 512x512 (tools/tune.py; profiles/tune_r1*.txt).
+//   16-bit: the 64-byte-row ring kernel; 128-row wave tiles on every layer with Cout >= 128
+//   (profiles/tune_r1_ring.txt), 3 taps per step on the 64-channel layers (tune_r1_ring_t3.txt),
+//   down1.0 fused into down1.3 (tune_r1_ring_fused_in.txt).
+//   fp32: the 128-byte LDS-halo kernel (tune_r1.txt).
+const int kRingCfg[17] = {
+    CFG_RING_FUSED_IN,                                  // down1.0 + down1.3 (+pool), fused
+    CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128,
+    CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128,
+    CFG_RING_R128, CFG_RING_R128,                       // down2.0 .. conv2.3
+    CFG_RING_R64_T3, CFG_RING_R64_T3};                  // conv1.0, conv1.3 (+head)
+const int kHaloCfg[17] = {
+    CFG_HALO_R64_W8,                                    // down1.3 (+pool)
+    CFG_HALO_R128, CFG_HALO_R128, CFG_HALO_R128, CFG_HALO_R64_W4, CFG_HALO_R128, CFG_HALO_R64_W4,
+    CFG_HALO_R128, CFG_HALO_R128, CFG_HALO_R128, CFG_HALO_R128, CFG_HALO_R128, CFG_HALO_R128,
+    CFG_HALO_R128, CFG_HALO_R128,                       // down2.0 .. conv2.3
+    CFG_HALO_R64_W4, CFG_HALO_R64_W8};                  // conv1.0, conv1.3 (+head)
 const char* kUpKey[4] = {"up4", "up3", "up2", "up1"};
 const int kUpCh[4][2] = {{1024, 512}, {512, 256}, {256, 128}, {128, 64}};
+
+// Storage precision of a level under the handle's dtype.  UNET_DTYPE_MIXED: fp16 at the two
+// full-resolution levels 0-1 (where the mask boundaries are decided), bf16 at levels 2-4.
+// Chosen by tools/numerics_emulate.py: bf16 everywhere gives a worst field IoU of 0.9983 against
+// the fp32 reference masks on the bench pages, fp16 at levels 0-1 0.9994, fp16 at level 0 only
+// 0.9990.  fp16 and bf16 run the same MFMA rate on gfx950.
+DType level_dtype(int dtype, int level) {
+  switch (dtype) {
+    case UNET_DTYPE_F32: return DType::F32;
+    case UNET_DTYPE_F16: return DType::F16;
+    case UNET_DTYPE_MIXED: return level <= 1 ? DType::F16 : DType::BF16;
+    default: return DType::BF16;
+  }
+}
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -165,7 +202,10 @@ Buffers plan(DType dt, int N, int H, int W) {
   b.tB = take(P / 4 * 128);
   b.mbits = o;   // bit-packed masks for unet_forward_boxes without caller masks (<= kMaxClasses fields)
   o = align256(o + (size_t)kMaxClasses * P / 8);
-  b.xpx = take(P * 4);   // network input as T [N][H][W][4] for the ring kernel's fused first conv
+  // network input in the first layer's format: T [N][H][W][4] (16-bit ring kernel's fused first
+  // conv) or fp32 NCHW (fp32 path, when the caller's input is not fp32 NCHW already)
+  b.xpx = o;
+  o = align256(o + P * (e == 2 ? 4 * 2 : 3 * 4));
   b.total = o;
   return b;
 }
@@ -240,9 +280,9 @@ void put_elem(DType dt, std::vector<uint8_t>& buf, size_t idx, double v) {
 // packed[((ct * S + s) * BR + rho % BR) * BKE + c % BKE], S = 9 * cin / BKE.
 int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::vector<double>& b) {
   const int K = 9 * L.cin;
-  std::vector<uint8_t> buf((size_t)L.cout * K * dtype_size(h->dt));
+  std::vector<uint8_t> buf((size_t)L.cout * K * dtype_size(L.dt));
   const bool ring = cfg_is_ring(L.cfg);
-  const int BR = cfg_rows(L.cfg), BKE = 64 / (int)dtype_size(h->dt), S = K / BKE;
+  const int BR = cfg_rows(L.cfg), BKE = 64 / (int)dtype_size(L.dt), S = K / BKE;
   if (ring && (L.cout % BR || L.cin % BKE)) return fail(UNET_EINVAL, "ring kernel tiling does not divide the layer");
   for (int rho = 0; rho < L.cout; ++rho) {
     const int o = natural_of_packed(rho);
@@ -250,7 +290,7 @@ int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::v
       for (int c = 0; c < L.cin; ++c) {
         const size_t idx = ring ? (((size_t)(rho / BR) * S + (size_t)(c / BKE) * 9 + tap) * BR + rho % BR) * BKE + c % BKE
                                 : (size_t)rho * K + (size_t)tap * L.cin + c;
-        put_elem(h->dt, buf, idx, w[((size_t)o * L.cin + c) * 9 + tap]);
+        put_elem(L.dt, buf, idx, w[((size_t)o * L.cin + c) * 9 + tap]);
       }
   }
   std::vector<float> bf(b.begin(), b.end());
@@ -259,14 +299,13 @@ int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::v
   return rc;
 }
 
-// ConvTranspose2d(k2,s2): natural GEMM row R = (a*2+b)*cout + o; packed[rho][c] = W[c][o][a][b]
-// ConvTranspose2d (Cin, Cout, 2, 2) as GEMM rows (a, b, o): packed[rho][c]; the ring kernel
-// (cfg_is_tring) takes them in step order per 128-row tile: [ct][c / BKE][BR][BKE].
+// ConvTranspose2d (Cin, Cout, 2, 2) as GEMM rows (a, b, o): packed[rho][c] = W[c][o][a][b]; the
+// ring kernel (cfg_is_tring) takes them in step order per BR-row tile: [ct][c / BKE][BR][BKE].
 int packT(unet_handle* h, Layer& L, const float* W, const float* B) {
   const int R = 4 * L.cout;
-  std::vector<uint8_t> buf((size_t)R * L.cin * dtype_size(h->dt));
+  std::vector<uint8_t> buf((size_t)R * L.cin * dtype_size(L.dt));
   const bool ring = cfg_is_tring(L.cfg);
-  const int BR = cfg_rows(L.cfg), BKE = 64 / (int)dtype_size(h->dt), S = L.cin / BKE;
+  const int BR = cfg_rows(L.cfg), BKE = 64 / (int)dtype_size(L.dt), S = L.cin / BKE;
   if (ring && (R % BR || L.cin % BKE)) return fail(UNET_EINVAL, "ring ConvTranspose tiling does not divide the layer");
   for (int rho = 0; rho < R; ++rho) {
     const int nat = natural_of_packed(rho);
@@ -274,7 +313,7 @@ int packT(unet_handle* h, Layer& L, const float* W, const float* B) {
     for (int c = 0; c < L.cin; ++c) {
       const size_t idx = ring ? (((size_t)(rho / BR) * S + c / BKE) * BR + rho % BR) * BKE + c % BKE
                               : (size_t)rho * L.cin + c;
-      put_elem(h->dt, buf, idx, W[(((size_t)c * L.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]);
+      put_elem(L.dt, buf, idx, W[(((size_t)c * L.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]);
     }
   }
   std::vector<float> bias(R);
@@ -284,11 +323,35 @@ int packT(unet_handle* h, Layer& L, const float* W, const float* B) {
   return rc;
 }
 
+// Make the next use of the shared workspace (and of the preprocess buffers) on `s` wait for the
+// previous call if that ran on another stream; unet_forward / unet_preprocess calls on different
+// streams are thus serialised on the device, not only on the host (the handle has ONE workspace).
+void order_after_last(unet_handle* h, hipStream_t s) {
+  if (!h->capturing && h->pending && h->last_stream != s) (void)hipStreamWaitEvent(s, h->done, 0);
+}
+void mark_done(unet_handle* h, hipStream_t s) {
+  if (!h->capturing && hipEventRecord(h->done, s) == hipSuccess) {
+    h->last_stream = s;
+    h->pending = true;
+  }
+}
+
+// Every device buffer that queued work may still read is freed only after that work.
+void drain(unet_handle* h) {
+  if (h->pending) (void)hipEventSynchronize(h->done);
+  h->pending = false;
+}
+
+void free_resample(ResampleStore& st) {
+  for (void* p : st.bufs) (void)hipFree(p);
+  st.bufs.clear();
+}
+
 void free_all(unet_handle* h) {
+  drain(h);
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
-  for (auto& kv : h->resample)
-    for (void* p : kv.second.bufs) (void)hipFree(p);
+  for (auto& kv : h->resample) free_resample(kv.second);
   h->resample.clear();
   if (h->pp_tmp) (void)hipFree(h->pp_tmp);
   h->pp_tmp = nullptr;
@@ -355,37 +418,24 @@ int check_geometry(const unet_handle* h, int N, int H, int W) {
   return UNET_OK;
 }
 
-}  // namespace
-
-namespace {
 const char* tname(DType t) { return t == DType::F32 ? "float" : t == DType::BF16 ? "__bf16" : "_Float16"; }
 
 // "kernel<template args>" of a layer, in the same spelling as the demangled symbol
-std::string layer_label(DType t, int cfg, int taps, int epi) {
-  char buf[128];
-  struct { int wr, wpx, tc, hb, ns, pipe; } halo[] = {
-      {2, 2, 4, 2, 3, 0}, {2, 4, 4, 2, 3, 0}, {1, 4, 4, 2, 3, 0}, {1, 8, 4, 2, 3, 0}, {1, 4, 4, 1, 3, 0},
-      {1, 8, 4, 1, 3, 0}, {2, 2, 4, 1, 2, 0}, {2, 4, 4, 2, 3, 1}, {1, 4, 4, 1, 3, 1}, {1, 8, 4, 1, 3, 1},
-      {1, 4, 8, 1, 2, 0}, {1, 4, 8, 1, 3, 0}, {1, 4, 4, 1, 3, 0}, {1, 8, 4, 1, 3, 0},
-      {1, 4, 4, 1, 3, 0}, {1, 4, 4, 2, 3, 0}, {1, 2, 4, 2, 3, 0}, {1, 8, 4, 3, 3, 0}, {1, 4, 4, 3, 3, 0},
-      {1, 4, 8, 1, 2, 7}, {1, 4, 8, 1, 3, 7}, {1, 4, 4, 1, 3, 7}, {1, 8, 4, 1, 3, 7}};
-  if (cfg >= CFG_COUNT) {
-    std::snprintf(buf, sizeof buf, "ablation_%d<%s, %d>", cfg - CFG_COUNT, tname(t), epi);
-  } else if (cfg_is_tring(cfg)) {
-    std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, %d, %d, %d>", tname(t), cfg == CFG_TRING_R256_NS4 ? 4 : 3,
-                  cfg == CFG_TRING_R128_CTI ? 1 : 0, cfg == CFG_TRING_R256 || cfg == CFG_TRING_R256_NS4 ? 2 : 1);
+std::string layer_label(const Layer& L, int epi) {
+  char buf[160];
+  const int cfg = L.cfg;
+  if (cfg_is_tring(cfg)) {
+    std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, %d, %d, %s>", tname(L.dt), cfg == CFG_TRING_R256 ? 4 : 3,
+                  cfg == CFG_TRING_R256 ? 2 : 1, tname(L.dto));
   } else if (cfg_is_ring(cfg)) {
-    const int tc = cfg_rows(cfg) / 16;
-    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, 0, %d, %d>", tname(t), tc, ring_ns(cfg),
-                  epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0);
-  } else if (cfg_is_halo(cfg)) {
-    const auto& c = halo[cfg - CFG_HALO_R128_W4];
-    const int hsrc = (cfg == CFG_FUSED_IN_W4 || cfg == CFG_FUSED_IN_W8) ? 1 : 0;
-    std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d>", tname(t), c.wr,
-                  c.wpx, c.tc, c.hb, c.ns, c.pipe, hsrc, taps == 9 ? 3 : 1, cfg_pixels(cfg) / 16, epi);
+    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %s, %s>", tname(L.dt),
+                  cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0,
+                  tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto));
   } else {
-    const int wr = cfg_rows(cfg) / 64, wpx = 4 / wr, tp = cfg_pixels(cfg) / (16 * wpx);
-    std::snprintf(buf, sizeof buf, "igemm_kernel<%s, %d, %d, %d, %d, %d>", tname(t), wr, wpx, tp, taps, epi);
+    const int wpx = cfg == CFG_HALO_R64_W8 ? 8 : 4, tc = cfg == CFG_HALO_R128 ? 8 : 4,
+              ns = cfg == CFG_HALO_R128 ? 2 : 3;
+    std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, 1, %d, %d, %d, %d, %d>", tname(L.dt), wpx, tc, ns,
+                  L.taps == 9 ? 3 : 1, epi);
   }
   return buf;
 }
@@ -393,25 +443,42 @@ std::string layer_label(DType t, int cfg, int taps, int epi) {
 void build_labels(unet_handle* h) {
   const int C = h->cfg.n_channels;
   char buf[96];
-  std::snprintf(buf, sizeof buf, h->dt == DType::F32 ? "first_conv_kernel<%s, %d>" : "first_conv_mfma_kernel<%s, %d>",
-                tname(h->dt), C);
+  const DType t0 = h->L[D1B].dt;
+  std::snprintf(buf, sizeof buf, t0 == DType::F32 ? "first_conv_kernel<%s, %d>" : "first_conv_mfma_kernel<%s, %d>",
+                tname(t0), C);
   // launch order (include/unet_mi355x.h): first, d1b .. bnb, up4, c4a, c4b, up3, c3a, c3b, up2, c2a, c2b, up1, c1a, c1b
   const int order[UNET_NUM_LAUNCHES] = {-1, D1B, D2A, D2B, D3A, D3B, D4A, D4B, BNA, BNB, 100, C4A, C4B,
                                         101, C3A, C3B, 102, C2A, C2B, 103, C1A, C1B};
   for (int i = 0; i < UNET_NUM_LAUNCHES; ++i) {
     const int id = order[i];
     if (id < 0) {
-      if (h->L[D1B].cfg == CFG_RING_FUSED_IN)
-        h->labels[i] = std::string("x_to_px4_kernel<") + tname(h->dt) + ">";   // pre-cast; conv fused into down1.3
-      else
-        h->labels[i] = is_fused_in(h->L[D1B].cfg) ? "fused_into_down1.3" : buf;
+      h->labels[i] = h->L[D1B].cfg == CFG_RING_FUSED_IN ? std::string("x_to_px4_kernel<") + tname(t0) + ">" : buf;
       continue;
     }
-    if (id >= 100) { h->labels[i] = layer_label(h->dt, h->U[id - 100].cfg, 1, EPI_UPSCATTER); continue; }
+    if (id >= 100) { h->labels[i] = layer_label(h->U[id - 100], EPI_UPSCATTER); continue; }
     const int epi = id == C1B ? EPI_HEAD : (id == D1B || id == D2B || id == D3B || id == D4B) ? EPI_POOL : EPI_STORE;
-    h->labels[i] = layer_label(h->dt, h->L[id].cfg, 9, epi);
+    h->labels[i] = layer_label(h->L[id], epi);
   }
 }
+
+// "layer:cfg,..." override list (tools/tune.py A/B runs)
+void parse_overrides(const char* ov, int n, int* cfg_out, bool (*ok)(int, int)) {
+  if (!ov) return;
+  std::string o(ov);
+  size_t pos = 0;
+  while (pos < o.size()) {
+    size_t end = o.find(',', pos);
+    if (end == std::string::npos) end = o.size();
+    const std::string item = o.substr(pos, end - pos);
+    const size_t colon = item.find(':');
+    if (colon != std::string::npos) {
+      const int li = std::atoi(item.substr(0, colon).c_str()), c = std::atoi(item.substr(colon + 1).c_str());
+      if (li >= 0 && li < n && c >= 0 && c < CFG_COUNT && ok(li, c)) cfg_out[li] = c;
+    }
+    pos = end + 1;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -439,7 +506,9 @@ float unet_logit_cut(float thr) {
   // The reference thresholds probabilities: torch.sigmoid(logits) > thr (inference.py:72-78).
   // The fp32 sigmoid is monotone non-decreasing in x, so that predicate is exactly
   // "x > cut" for the largest float cut at which it is still false; the masks kernel
-  // compares logits against the cut and never evaluates exp.
+  // compares logits against the cut and never evaluates exp.  The cut is bisected with the
+  // host libm expf; torch's sigmoid (Sleef on CPU, ocml on ROCm) may round a logit within an
+  // ulp or two of the cut differently (tests/test_forward_gpu.py::test_logit_cut_matches_torch_sigmoid).
   const float inf = INFINITY;
   long long lo = float_key(-inf), hi = float_key(inf);
   if (sigmoid_above(-inf, thr)) return -inf;        // every logit passes
@@ -456,100 +525,59 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   if (!cfg || !out) return fail(UNET_EINVAL, "null argument");
   if (cfg->n_channels != 1 && cfg->n_channels != 3) return fail(UNET_EINVAL, "n_channels must be 1 or 3");
   if (cfg->n_classes < 1 || cfg->n_classes > kMaxClasses) return fail(UNET_EINVAL, "n_classes must be 1..4");
-  if (cfg->dtype < 0 || cfg->dtype > 2) return fail(UNET_EINVAL, "bad dtype");
+  if (cfg->dtype < 0 || cfg->dtype > UNET_DTYPE_MIXED) return fail(UNET_EINVAL, "bad dtype");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (cfg->device < 0 || cfg->device >= ndev) return fail(UNET_EINVAL, "bad device ordinal");
   unet_handle* h = new unet_handle();
   h->cfg = *cfg;
-  h->dt = (DType)cfg->dtype;
+  const bool f32 = cfg->dtype == UNET_DTYPE_F32;
+  h->dt = f32 ? DType::F32 : DType::BF16;   // workspace element size (all 16-bit plans: 2 bytes)
   for (int i = 0; i < kMaxClasses; ++i) h->thr_logit[i] = unet_logit_cut(cfg->thresholds[i]);
-  // Kernel configuration per layer (tuned on MI355X).  Overrides for
-  // tuning / A-B runs: UNET_MI355X_PRESET=gather (first-generation per-tap kernel for
-  // every layer) and UNET_MI355X_CFG="layer:cfg,..." (layer = index into L[], cfg = Cfg).
-  const char* preset = std::getenv("UNET_MI355X_PRESET");
-  const std::string ps = preset ? preset : "";
-  const int chunk = cfg->dtype == UNET_DTYPE_F32 ? 32 : 64;   // channels per 128-byte chunk
+  // Kernel configuration per layer (tuned on MI355X).  A/B override for tuning:
+  // UNET_MI355X_CFG="layer:cfg,..." (layer = index into L[], cfg = Cfg) and
+  // UNET_MI355X_UPCFG="i:cfg,..." (i = 0..3 = up4..up1).
+  int cfgs[17], ucfgs[4];
+  for (int i = 0; i < 17; ++i) cfgs[i] = f32 ? kHaloCfg[i] : kRingCfg[i];
+  for (int i = 0; i < 4; ++i) ucfgs[i] = f32 ? (int)CFG_HALO_R128 : (int)CFG_TRING_R256;
+  parse_overrides(std::getenv("UNET_MI355X_CFG"), 17, cfgs, [](int, int c) { return cfg_is_halo(c) || cfg_is_ring(c); });
+  parse_overrides(std::getenv("UNET_MI355X_UPCFG"), 4, ucfgs, [](int, int c) { return cfg_is_tring(c) || c == CFG_HALO_R128; });
   for (int i = 0; i < 17; ++i) {
     Layer& L = h->L[i];
     L.cin = kLayerCh[i][0];
     L.cout = L.ctot = kLayerCh[i][1];
     L.taps = 9;
-    if (ps == "gather") {
-      L.cfg = L.cout == 64 ? CFG_R64_P256 : CFG_R128_P128;
-    } else {
-      // 16-bit: the 64-byte-row ring kernel on the 128-row layers (A/B: profiles/tune_r1_ring.txt);
-      // fp32 stays on the 128-byte halo kernel
-      L.cfg = cfg->dtype == UNET_DTYPE_F32 ? kDefaultCfg[i]
-              : (i >= 1 && i <= 14) ? (int)CFG_RING_R128_NS3 : (i == C1A || i == C1B) ? (int)CFG_RING_R64_T3
-              : (i == D1B) ? (int)CFG_RING_FUSED_IN : kDefaultCfg[i];
-    }
-  }
-  if (ps == "gather") h->L[C1B].cfg = CFG_R64_P128;
-  if (const char* ov = std::getenv("UNET_MI355X_CFG")) {
-    std::string o(ov);
-    size_t pos = 0;
-    while (pos < o.size()) {
-      size_t end = o.find(',', pos);
-      if (end == std::string::npos) end = o.size();
-      const std::string item = o.substr(pos, end - pos);
-      const size_t colon = item.find(':');
-      if (colon != std::string::npos) {
-        const int li = std::atoi(item.substr(0, colon).c_str()), c = std::atoi(item.substr(colon + 1).c_str());
-        if (li >= 0 && li < 17 && c >= 0 && c < cfg_limit() && !cfg_is_tring(c)) h->L[li].cfg = c;
-      }
-      pos = end + 1;
-    }
-  }
-  for (int i = 0; i < 17; ++i) {   // keep every layer on a configuration it supports
-    Layer& L = h->L[i];
-    const bool fused_in = is_fused_in(L.cfg);
-    // fall back within the same kernel family (LDS-halo configurations all accumulate in the
-    // same K order, so they agree bitwise; the gather kernels order K differently)
-    // (the ring kernels share one K order among themselves, chunk32-major)
-    const bool ring = cfg_is_ring(L.cfg);
-    const bool halo = cfg_is_halo(L.cfg) && !ring;
-    if (fused_in && (i != D1B || cfg->dtype == UNET_DTYPE_F32))
-      L.cfg = L.cfg == CFG_RING_FUSED_IN ? (L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128_NS3)
-                                         : (L.cout == 64 ? CFG_HALO1_R64_W8 : CFG_HALO1_R128T8_NS2);
-    if (cfg_rows(L.cfg) > L.cout || L.cfg == CFG_R128_P256 || (cfg_single_chunk(L.cfg) && L.cin != chunk))
-      L.cfg = L.cout == 64 ? (ring ? CFG_RING_R64 : halo ? CFG_HALO1_R64_W8 : CFG_R64_P256)
-                           : (ring ? CFG_RING_R128_NS3 : halo ? CFG_HALO1_R128T8_NS2 : CFG_R128_P128);
-    if (i == C1B && cfg_rows(L.cfg) != 64) L.cfg = ring ? CFG_RING_R64 : halo ? CFG_HALO1_R64_W8 : CFG_R64_P128;
+    L.dt = L.dto = level_dtype(cfg->dtype, kLayerLevel[i]);
+    L.dtq = level_dtype(cfg->dtype, kLayerLevel[i] + 1);
+    int c = cfgs[i];
+    // keep every layer on a configuration it supports, within the same kernel family (the
+    // configurations of a family accumulate in the same K order, so they agree bitwise)
+    const bool ring = cfg_is_ring(c);
+    if (c == CFG_RING_FUSED_IN && (i != D1B || f32)) c = L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128;
+    if (cfg_rows(c) > L.cout || (i == C1B && cfg_rows(c) != 64))
+      c = ring ? CFG_RING_R64_T3 : CFG_HALO_R64_W8;
+    // the LDS-halo family stores its own operand type only: keep it off the mixed plan's seams
+    const bool pool = i == D1B || i == D2B || i == D3B || i == D4B;
+    if (cfg_is_halo(c) && (L.dto != L.dt || (pool && L.dtq != L.dt))) c = L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128;
+    L.cfg = c;
   }
   for (int i = 0; i < 4; ++i) {
-    h->U[i].cin = kUpCh[i][0];
-    h->U[i].cout = kUpCh[i][1];
-    h->U[i].ctot = 4 * kUpCh[i][1];
-    h->U[i].taps = 1;
-    h->U[i].cfg = ps == "gather" ? CFG_R128_P128 : (cfg->dtype == UNET_DTYPE_F32 ? kDefaultUpCfg[i] : (int)CFG_TRING_R256_NS4);
-  }
-  if (const char* ov = std::getenv("UNET_MI355X_UPCFG")) {   // "i:cfg,..." i = 0..3 (up4..up1)
-    std::string o(ov);
-    size_t pos = 0;
-    while (pos < o.size()) {
-      size_t end = o.find(',', pos);
-      if (end == std::string::npos) end = o.size();
-      const std::string item = o.substr(pos, end - pos);
-      const size_t colon = item.find(':');
-      if (colon != std::string::npos) {
-        const int li = std::atoi(item.substr(0, colon).c_str()), c = std::atoi(item.substr(colon + 1).c_str());
-        if (li >= 0 && li < 4 && (c == CFG_R128_P128 || c == CFG_R64_P128 || c == CFG_HALO1_R64_W4 ||
-                                  c == CFG_HALO1_R128T8_NS2 || c == CFG_HALO_R128_W8 || c == CFG_HALO1_R64_W8 ||
-                                  c == CFG_HALO1_R128T8_NS3 || c == CFG_HALO_R128_W4 || c == CFG_HALO3_R64_W8 ||
-                                  c == CFG_HALO3_R64_W4 || c == CFG_SG_R128T8_NS2 || c == CFG_SG_R64_W4 ||
-                                  c == CFG_TRING_R128 || c == CFG_TRING_R128_CTI || c == CFG_TRING_R256 ||
-                                  c == CFG_TRING_R256_NS4))
-          h->U[li].cfg = c;
-      }
-      pos = end + 1;
-    }
+    Layer& U = h->U[i];
+    U.cin = kUpCh[i][0];
+    U.cout = kUpCh[i][1];
+    U.ctot = 4 * kUpCh[i][1];
+    U.taps = 1;
+    U.dt = level_dtype(cfg->dtype, kUpLevel[i]);
+    U.dto = U.dtq = level_dtype(cfg->dtype, kUpLevel[i] - 1);
+    U.cfg = (ucfgs[i] == CFG_HALO_R128 && U.dto != U.dt) ? (int)CFG_TRING_R256 : ucfgs[i];
   }
   build_labels(h);   // after every layer's configuration (3x3 and ConvTranspose) is final
   DeviceGuard g(cfg->device);
+  hipError_t e = hipEventCreateWithFlags(&h->done, hipEventDisableTiming);
+  if (e != hipSuccess) { delete h; return fail(UNET_EHIP, std::string("hipEventCreate: ") + hipGetErrorString(e)); }
   std::vector<uint8_t> z(256, 0);
   int rc = upload(h, &h->zero, z.data(), z.size());
-  if (rc) { free_all(h); delete h; return rc; }
+  if (rc) { free_all(h); (void)hipEventDestroy(h->done); delete h; return rc; }
   *out = h;
   return UNET_OK;
 }
@@ -567,7 +595,8 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
     return fail(UNET_EKEY, "state_dict has " + std::to_string(sd.m.size()) + " keys, expected " +
                                std::to_string(expected));
   DeviceGuard g(h->cfg.device);
-  // drop previously loaded weights (keep the zero page)
+  drain(h);   // in-flight forwards may still read the weights about to be freed
+  ++h->generation;
   for (void* p : h->allocs)
     if (p != h->zero) (void)hipFree(p);
   h->allocs.assign(1, h->zero);
@@ -584,20 +613,22 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
     if (rc) return rc;
     h->w0p = nullptr;
     h->w0r = nullptr;
-    if (h->dt != DType::F32) {   // MFMA operand: [rho][k], k = c*9 + ky*3 + kx < 9C, zero pad to 32
+    const DType t0 = h->L[D1B].dt;
+    if (t0 != DType::F32) {   // MFMA operand: [rho][k], k = c*9 + ky*3 + kx < 9C, zero pad to 32
       std::vector<uint8_t> pk((size_t)64 * 32 * 2, 0);
       for (int rho = 0; rho < 64; ++rho) {
         const int o = natural_of_packed(rho);
-        for (int k = 0; k < 9 * C; ++k) put_elem(h->dt, pk, (size_t)rho * 32 + k, w[(size_t)o * 9 * C + k]);
+        for (int k = 0; k < 9 * C; ++k) put_elem(t0, pk, (size_t)rho * 32 + k, w[(size_t)o * 9 * C + k]);
       }
       rc = upload(h, &h->w0p, pk.data(), pk.size());
       if (rc) return rc;
       std::vector<uint8_t> pr((size_t)64 * 32 * 2, 0);
       for (int cb = 0; cb < 2; ++cb)
-        for (int t = 0; t < 2; ++t)
+        for (int tt = 0; tt < 2; ++tt)
           for (int r = 0; r < 16; ++r) {
-            const int o = 32 * cb + 8 * (r >> 2) + 4 * t + (r & 3);
-            for (int k = 0; k < 9 * C; ++k) put_elem(h->dt, pr, ((size_t)(cb * 2 + t) * 16 + r) * 32 + k, w[(size_t)o * 9 * C + k]);
+            const int o = 32 * cb + 8 * (r >> 2) + 4 * tt + (r & 3);
+            for (int k = 0; k < 9 * C; ++k)
+              put_elem(t0, pr, ((size_t)(cb * 2 + tt) * 16 + r) * 32 + k, w[(size_t)o * 9 * C + k]);
           }
       rc = upload(h, &h->w0r, pr.data(), pr.size());
       if (rc) return rc;
@@ -640,8 +671,9 @@ int unet_reserve(unet_handle* h, int N, int H, int W) {
   const size_t need = plan(h->dt, N, H, W).total;
   if (need <= h->ws_bytes) return UNET_OK;
   DeviceGuard g(h->cfg.device);
+  ++h->generation;
   if (h->ws) {
-    HIP_TRY(hipDeviceSynchronize());
+    drain(h);   // the old workspace may still be in use by queued forwards
     (void)hipFree(h->ws);
     h->ws = nullptr;
     h->ws_bytes = 0;
@@ -678,71 +710,39 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.ldo = ldo; a.out_off = out_off; a.ldo2 = ldo2;
   a.ncls = h->cfg.n_classes;
   a.mask_kind = mask_kind;
-  if (is_fused_in(L.cfg)) {
+  if (L.cfg == CFG_RING_FUSED_IN) {
     a.x0 = x0;
-    a.w0p = L.cfg == CFG_RING_FUSED_IN ? h->w0r : h->w0p;
+    a.w0p = h->w0r;
     a.b0 = h->b0;
     a.c0 = h->cfg.n_channels;
   }
   for (int i = 0; i < kMaxClasses; ++i) a.thr_logit[i] = h->thr_logit[i];
-  const int BR = cfg_rows(L.cfg), BP = cfg_pixels(L.cfg);
-  const int TH = BP / 16;
   a.tiles_x = (W + 15) / 16;
-  a.tiles_y = (H + TH - 1) / TH;
-  a.n_ct = L.ctot / BR;
-  const long long nb = (long long)N * a.tiles_x * a.tiles_y * a.n_ct;
-  if (nb <= 0 || nb > 0x7FFFFFFFLL) return fail(UNET_ESHAPE, "grid too large");
-  a.n_blocks = (int)nb;
-#ifdef UNET_ABLATION
-  // diagnostic build: stamped configurations report a per-wave cycle breakdown on stderr
-  static unsigned long long* dbg = nullptr;
-  const bool stamped = L.cfg >= CFG_COUNT + 7 && L.cfg <= CFG_COUNT + 10;
-  const size_t dbg_n = (size_t)16 * 1024 * 1024;
-  if (stamped && !dbg) (void)hipMalloc((void**)&dbg, dbg_n * 8);
-  if (stamped && dbg) {
-    (void)hipMemsetAsync(dbg, 0, dbg_n * 8, s);
-    a.dbg = dbg;
-  }
-#endif
-  hipError_t e = launch_igemm(h->dt, L.cfg, L.taps, epi, a, s);
+  a.tiles_y = (H + 15) / 16;
+  a.n_ct = L.ctot / cfg_rows(L.cfg);
+  hipError_t e = launch_igemm(L.dt, L.dto, epi == EPI_POOL ? L.dtq : L.dto, L.cfg, L.taps, epi, a, s);
   if (e != hipSuccess) return fail(UNET_EHIP, std::string("igemm launch: ") + hipGetErrorString(e));
-#ifdef UNET_ABLATION
-  if (stamped && dbg) {
-    (void)hipStreamSynchronize(s);
-    std::vector<unsigned long long> hbuf(dbg_n);
-    (void)hipMemcpy(hbuf.data(), dbg, dbg_n * 8, hipMemcpyDeviceToHost);
-    double sum[6] = {0, 0, 0, 0, 0, 0};
-    size_t cnt = 0;
-    for (size_t i = 0; i + 8 <= dbg_n; i += 8)
-      if (hbuf[i + 6]) { for (int k = 0; k < 6; ++k) sum[k] += (double)hbuf[i + k]; ++cnt; }
-    if (cnt)
-      std::fprintf(stderr, "[stamp] cfg %d Cin %d Cout %d HxW %dx%d waves %zu: avg cycles/wave prologue %.0f "
-                   "compute %.0f wait %.0f epilogue %.0f total %.0f steps %.1f\n", L.cfg, L.cin, L.cout, H, W, cnt,
-                   sum[0] / cnt, sum[1] / cnt, sum[2] / cnt, sum[3] / cnt, sum[4] / cnt, sum[5] / cnt);
-  }
-#endif
   return UNET_OK;
 }
 
-}  // namespace
-
-namespace {
 // The launch sequence of UNet.forward (unet_model.py:55-86).  ev (optional, kLaunches+1
 // events) brackets every launch for per-layer timing.
 int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
                  int mask_kind, int32_t* boxes, int N, int H, int W, void* stream, hipEvent_t* ev) {
   if (!h || !x) return fail(UNET_EINVAL, "null argument");
   if (!h->loaded) return fail(UNET_ESTATE, "weights not loaded");
-  if (x_layout != UNET_LAYOUT_NCHW || x_dtype != UNET_IN_F32)
-    return fail(UNET_EINVAL, "only fp32 NCHW input is supported");
+  if ((x_layout != UNET_LAYOUT_NCHW && x_layout != UNET_LAYOUT_NHWC) || (x_dtype != UNET_IN_F32 && x_dtype != UNET_IN_U8))
+    return fail(UNET_EINVAL, "x_layout must be UNET_LAYOUT_NCHW / NHWC and x_dtype UNET_IN_F32 / U8");
   if (mask_kind < 0 || mask_kind > 2) return fail(UNET_EINVAL, "bad mask_kind");
   if (mask_kind != UNET_MASK_NONE && !masks) return fail(UNET_EINVAL, "mask_kind set but masks is NULL");
   int rc = check_geometry(h, N, H, W);
   if (rc) return rc;
-  rc = unet_reserve(h, N, H, W);
-  if (rc) return rc;
+  // no allocation (and so no hidden device synchronisation) here: unet_reserve sizes the workspace
+  if (plan(h->dt, N, H, W).total > h->ws_bytes)
+    return fail(UNET_ESTATE, "workspace too small for this (N, H, W): call unet_reserve first");
   DeviceGuard g(h->cfg.device);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  order_after_last(h, s);
   const Buffers B = plan(h->dt, N, H, W);
   char* ws = h->ws;
   auto buf = [&](size_t off) { return static_cast<void*>(ws + off); };
@@ -751,26 +751,33 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
     mask_kind = UNET_MASK_BITS;
   }
   const int H2 = H / 2, W2 = W / 2, H4 = H / 4, W4 = W / 4, H8 = H / 8, W8 = W / 8, H16 = H / 16, W16 = W / 16;
+  const int C = h->cfg.n_channels;
 
-  // down1.net.0 (C -> 64): direct conv
-  FirstConvArgs f{};
-  f.x = static_cast<const float*>(x);
-  f.w = h->w0;
-  f.wp = h->w0p;
-  f.b = h->b0;
-  f.out = buf(B.tA);
-  f.N = N; f.C = h->cfg.n_channels; f.H = H; f.W = W;
   int li = 0;
   auto mark = [&]() { if (ev) (void)hipEventRecord(ev[li], s); ++li; };
   mark();
-  const bool fused_in = is_fused_in(h->L[D1B].cfg);   // down1.0 computed inside down1.3
+  // down1.net.0 (C -> 64): fused into down1.3 on the 16-bit ring path (fed by the pre-cast input),
+  // a direct conv otherwise
   const void* x0 = x;
-  if (h->L[D1B].cfg == CFG_RING_FUSED_IN) {   // the ring's fused first conv reads T [N][H][W][4]
-    hipError_t e = launch_x_to_px4(h->dt, static_cast<const float*>(x), N, h->cfg.n_channels, H, W, buf(B.xpx), s);
+  if (h->L[D1B].cfg == CFG_RING_FUSED_IN) {
+    hipError_t e = launch_x_to_px4(h->L[D1B].dt, x, x_layout, x_dtype, N, C, H, W, buf(B.xpx), s);
     if (e != hipSuccess) return fail(UNET_EHIP, std::string("input pre-cast launch: ") + hipGetErrorString(e));
     x0 = buf(B.xpx);
-  } else if (!fused_in) {
-    hipError_t e = launch_first_conv(h->dt, f, s);
+  } else {
+    const float* xf = static_cast<const float*>(x);
+    if (x_layout != UNET_LAYOUT_NCHW || x_dtype != UNET_IN_F32) {
+      hipError_t e = launch_x_to_nchw_f32(x, x_layout, x_dtype, N, C, H, W, static_cast<float*>(buf(B.xpx)), s);
+      if (e != hipSuccess) return fail(UNET_EHIP, std::string("input conversion launch: ") + hipGetErrorString(e));
+      xf = static_cast<const float*>(buf(B.xpx));
+    }
+    FirstConvArgs f{};
+    f.x = xf;
+    f.w = h->w0;
+    f.wp = h->w0p;
+    f.b = h->b0;
+    f.out = buf(B.tA);
+    f.N = N; f.C = C; f.H = H; f.W = W;
+    hipError_t e = launch_first_conv(h->L[D1B].dt, f, s);
     if (e != hipSuccess) return fail(UNET_EHIP, std::string("first conv launch: ") + hipGetErrorString(e));
   }
 
@@ -809,6 +816,7 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
     if (e != hipSuccess) return fail(UNET_EHIP, std::string("mask boxes launch: ") + hipGetErrorString(e));
   }
   mark();
+  mark_done(h, s);
   h->lastN = N; h->lastH = H; h->lastW = W;
   return UNET_OK;
 }
@@ -832,9 +840,18 @@ int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channel
   if (ih <= 0 || iw <= 0 || oh <= 0 || ow <= 0 || (long long)ih * iw > (1LL << 30) || oh > 16384 || ow > 16384)
     return fail(UNET_EINVAL, "bad image or output size");
   DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
   const auto key = std::make_tuple(ih, iw, oh, ow);
-  auto it = h->resample.find(key);
-  if (it == h->resample.end()) {
+  auto it = h->resample.begin();
+  while (it != h->resample.end() && it->first != key) ++it;
+  if (it != h->resample.end()) {
+    h->resample.splice(h->resample.begin(), h->resample, it);   // most recently used first
+  } else {
+    if (h->resample.size() >= kResampleCacheMax) {   // evict the least recently used geometry
+      drain(h);
+      free_resample(h->resample.back().second);
+      h->resample.pop_back();
+    }
     ResampleStore st;
     ResamplePlan& p = st.plan;
     p.ih = ih; p.iw = iw; p.oh = oh; p.ow = ow;
@@ -857,20 +874,25 @@ int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channel
       const size_t bytes = src[i]->size() * sizeof(int);
       hipError_t e = hipMalloc(&d, bytes);
       if (e != hipSuccess) {
-        for (void* q : st.bufs) (void)hipFree(q);
+        free_resample(st);
         return fail(UNET_ENOMEM, std::string("resample tables: ") + hipGetErrorString(e));
       }
       st.bufs.push_back(d);
-      HIP_TRY(hipMemcpy(d, src[i]->data(), bytes, hipMemcpyHostToDevice));
+      e = hipMemcpy(d, src[i]->data(), bytes, hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        free_resample(st);
+        return fail(UNET_EHIP, std::string("resample tables upload: ") + hipGetErrorString(e));
+      }
       *dst[i] = static_cast<const int*>(d);
     }
-    it = h->resample.emplace(key, std::move(st)).first;
+    h->resample.emplace_front(key, std::move(st));
+    it = h->resample.begin();
   }
   const ResamplePlan& p = it->second.plan;
   const size_t tmp = p.need_h ? (size_t)p.h_rows * ow * channels : 0;
   if (tmp > h->pp_tmp_bytes) {
     if (h->pp_tmp) {
-      HIP_TRY(hipDeviceSynchronize());
+      drain(h);
       (void)hipFree(h->pp_tmp);
       h->pp_tmp = nullptr;
       h->pp_tmp_bytes = 0;
@@ -879,9 +901,10 @@ int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channel
     if (e != hipSuccess) return fail(UNET_ENOMEM, std::string("preprocess buffer: ") + hipGetErrorString(e));
     h->pp_tmp_bytes = tmp;
   }
-  hipError_t e = launch_resample(p, static_cast<const uint8_t*>(img), channels, h->pp_tmp, x,
-                                 static_cast<hipStream_t>(stream));
+  order_after_last(h, s);
+  hipError_t e = launch_resample(p, static_cast<const uint8_t*>(img), channels, h->pp_tmp, x, s);
   if (e != hipSuccess) return fail(UNET_EHIP, std::string("resample launch: ") + hipGetErrorString(e));
+  mark_done(h, s);
   return UNET_OK;
 }
 
@@ -912,26 +935,89 @@ int unet_debug_fetch(unet_handle* h, const char* name, float* dst, size_t* numel
   if (!h->lastN) return fail(UNET_ESTATE, "no forward has run");
   const int N = h->lastN, H = h->lastH, W = h->lastW;
   const Buffers B = plan(h->dt, N, H, W);
-  struct Src { size_t off; int div, C, ld, choff; };
+  struct Src { size_t off; int level, C, ld, choff; };
   static const std::map<std::string, int> idx = {
       {"c1", 0}, {"p1", 1}, {"c2", 2}, {"p2", 3}, {"c3", 4}, {"p3", 5}, {"c4", 6}, {"p4", 7},
       {"bn", 8}, {"c7", 9}, {"u1", 10}, {"u2", 11}, {"u3", 12}, {"u4", 13}, {"c8a", 14}};
   auto it = idx.find(name);
   if (it == idx.end()) return fail(UNET_EINVAL, std::string("unknown intermediate ") + name);
-  const Src table[] = {{B.cat1, 1, 64, 128, 64},   {B.p1, 2, 64, 64, 0},     {B.cat2, 2, 128, 256, 128},
-                       {B.p2, 4, 128, 128, 0},     {B.cat3, 4, 256, 512, 256}, {B.p3, 8, 256, 256, 0},
-                       {B.cat4, 8, 512, 1024, 512}, {B.p4, 16, 512, 512, 0},  {B.bnb, 16, 1024, 1024, 0},
-                       {B.tB, 2, 128, 128, 0},     {B.cat1, 1, 64, 128, 0},  {B.cat2, 2, 128, 256, 0},
-                       {B.cat3, 4, 256, 512, 0},   {B.cat4, 8, 512, 1024, 0}, {B.tA, 1, 64, 64, 0}};
+  const Src table[] = {{B.cat1, 0, 64, 128, 64},   {B.p1, 1, 64, 64, 0},     {B.cat2, 1, 128, 256, 128},
+                       {B.p2, 2, 128, 128, 0},     {B.cat3, 2, 256, 512, 256}, {B.p3, 3, 256, 256, 0},
+                       {B.cat4, 3, 512, 1024, 512}, {B.p4, 4, 512, 512, 0},  {B.bnb, 4, 1024, 1024, 0},
+                       {B.tB, 1, 128, 128, 0},     {B.cat1, 0, 64, 128, 0},  {B.cat2, 1, 128, 256, 0},
+                       {B.cat3, 2, 256, 512, 0},   {B.cat4, 3, 512, 1024, 0}, {B.tA, 0, 64, 64, 0}};
   const Src& t = table[it->second];
-  const int h_ = H / t.div, w_ = W / t.div;
+  const int h_ = H >> t.level, w_ = W >> t.level;
   const size_t cnt = (size_t)N * t.C * h_ * w_;
   if (numel) *numel = cnt;
   if (!dst) return UNET_OK;
   DeviceGuard g(h->cfg.device);
-  hipError_t e = launch_nhwc_to_nchw_f32(h->dt, h->ws + t.off, N, h_, w_, t.C, t.ld, t.choff, dst,
-                                         static_cast<hipStream_t>(stream));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  order_after_last(h, s);
+  // each buffer holds its consumer's operand type (the mixed plan: fp16 at levels 0-1)
+  hipError_t e = launch_nhwc_to_nchw_f32(level_dtype(h->cfg.dtype, t.level), h->ws + t.off, N, h_, w_, t.C, t.ld,
+                                         t.choff, dst, s);
   if (e != hipSuccess) return fail(UNET_EHIP, std::string("debug fetch: ") + hipGetErrorString(e));
+  mark_done(h, s);
+  return UNET_OK;
+}
+
+int unet_graph_create(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
+                      int mask_kind, int32_t* boxes, int N, int H, int W, unet_graph** out) {
+  if (!h || !out) return fail(UNET_EINVAL, "null argument");
+  DeviceGuard g(h->cfg.device);
+  hipStream_t cs = nullptr;
+  HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  unet_graph* gr = new unet_graph();
+  gr->h = h;
+  hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+  int rc = UNET_OK;
+  if (e != hipSuccess) {
+    rc = fail(UNET_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
+  } else {
+    h->capturing = true;
+    rc = boxes ? forward_impl(h, x, x_layout, x_dtype, logits, masks, mask_kind, boxes, N, H, W, cs, nullptr)
+               : forward_impl(h, x, x_layout, x_dtype, logits, masks, mask_kind, nullptr, N, H, W, cs, nullptr);
+    h->capturing = false;
+    e = hipStreamEndCapture(cs, &gr->graph);
+    if (!rc && e != hipSuccess) rc = fail(UNET_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    if (!rc) {
+      e = hipGraphInstantiate(&gr->exec, gr->graph, nullptr, nullptr, 0);
+      if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+    }
+  }
+  (void)hipStreamDestroy(cs);
+  if (rc) {
+    if (gr->exec) (void)hipGraphExecDestroy(gr->exec);
+    if (gr->graph) (void)hipGraphDestroy(gr->graph);
+    delete gr;
+    return rc;
+  }
+  gr->generation = h->generation;
+  *out = gr;
+  return UNET_OK;
+}
+
+int unet_graph_launch(unet_graph* gr, void* stream) {
+  if (!gr || !gr->exec) return fail(UNET_EINVAL, "null graph");
+  unet_handle* h = gr->h;
+  if (gr->generation != h->generation)
+    return fail(UNET_ESTATE, "graph is stale: the handle's weights or workspace were re-allocated after capture");
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  order_after_last(h, s);
+  HIP_TRY(hipGraphLaunch(gr->exec, s));
+  mark_done(h, s);
+  return UNET_OK;
+}
+
+int unet_graph_destroy(unet_graph* gr) {
+  if (!gr) return UNET_OK;
+  DeviceGuard g(gr->h->cfg.device);
+  drain(gr->h);
+  if (gr->exec) (void)hipGraphExecDestroy(gr->exec);
+  if (gr->graph) (void)hipGraphDestroy(gr->graph);
+  delete gr;
   return UNET_OK;
 }
 
@@ -939,8 +1025,8 @@ int unet_destroy(unet_handle* h) {
   if (!h) return UNET_OK;
   {
     DeviceGuard g(h->cfg.device);
-    (void)hipDeviceSynchronize();
     free_all(h);
+    if (h->done) (void)hipEventDestroy(h->done);
   }
   delete h;
   return UNET_OK;

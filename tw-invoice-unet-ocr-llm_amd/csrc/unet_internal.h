@@ -45,14 +45,13 @@ struct IgemmArgs {
   int ldo, out_off, ldo2;
   int ncls, mask_kind;
   float thr_logit[kMaxClasses];   // logit cut per class: sigmoid(x) > thr  <=>  x > thr_logit
-  int tiles_x, tiles_y, n_ct, n_blocks;
+  int tiles_x, tiles_y, n_ct;
   // fused first conv (halo computed from the raw input instead of loaded): down1.0 + down1.3
   const void* x0;      // network input: NCHW fp32 [N][c0][H][W] (halo kernel), or T [N][H][W][4]
                        // (CFG_RING_FUSED_IN, see launch_x_to_px4)
   const void* w0p;     // first conv packed [64][32] element type (rows permuted)
   const float* b0;     // first conv folded bias [64]
   int c0;              // network input channels (1 or 3)
-  unsigned long long* dbg;   // diagnostic (ablation build) per-wave cycle stamps, or nullptr
 };
 
 struct FirstConvArgs {
@@ -65,55 +64,40 @@ struct FirstConvArgs {
   int N, C, H, W;
 };
 
-// Kernel configurations (rows tile x pixel tile).
-// CFG_R*_P*: per-tap gathered B tile (rows x pixels, tile 16 px wide); CFG_HALO_*: 16x16
-// pixel tile with an LDS halo (3x3 only), R = rows per block, W = waves per block.
+// Kernel configurations.  The LDS-halo family (128-byte K chunks, one tile per block) is the
+// fp32 path; the 64-byte-row ring family (persistent walkers, double-buffered halo, weight ring;
+// K order chunk32-major / tap-minor) is the 16-bit path; the ConvTranspose ring runs the 2x
+// upsamplers.  Selection per layer: unet_capi.cpp (defaults tuned on MI355X, profiles/tune_r1*).
 enum Cfg : int {
-  CFG_R128_P128 = 0, CFG_R64_P128 = 1, CFG_R64_P256 = 2, CFG_R128_P256 = 3,
-  CFG_HALO_R128_W4 = 4, CFG_HALO_R128_W8 = 5, CFG_HALO_R64_W4 = 6, CFG_HALO_R64_W8 = 7,
-  CFG_HALO1_R64_W4 = 8, CFG_HALO1_R64_W8 = 9,   // single halo buffer, two blocks per CU
-  CFG_HALO1_R128_W4 = 10,                       // single halo buffer, 2-slot weight ring
-  // software-pipelined fragment reads (next kk / next step read behind the MFMAs)
-  CFG_PHALO_R128_W8 = 11, CFG_PHALO1_R64_W4 = 12, CFG_PHALO1_R64_W8 = 13,
-  // 128-row x 64-pixel wave tiles (4 waves, 128 x 256 block), single halo buffer
-  CFG_HALO1_R128T8_NS2 = 14, CFG_HALO1_R128T8_NS3 = 15,
-  // down1.3 with down1.0 fused: the 18x18x64 halo is computed from the raw input (16-bit)
-  CFG_FUSED_IN_W4 = 16, CFG_FUSED_IN_W8 = 17,
-  // 8x16 pixel tiles (10x18 halo, 23 KB): HB=1 -> 3 blocks per CU; HB=2 persistent -> 2 per CU
-  CFG_T8_HALO1_R64_W4 = 18, CFG_T8_HALO_R64_W4 = 19, CFG_T8_HALO_R64_W2 = 20,
-  // persistent, 3-deep halo ring (two chunks / tiles of HBM loads in flight per CU)
-  CFG_HALO3_R64_W8 = 21, CFG_HALO3_R64_W4 = 22,
-  // single halo buffer with the fixed read/MFMA interleave (PIPE 7, sched_group_barrier)
-  CFG_SG_R128T8_NS2 = 23, CFG_SG_R128T8_NS3 = 24, CFG_SG_R64_W4 = 25, CFG_SG_R64_W8 = 26,
-  // 32-channel (64-byte-row) K chunks: double-buffered halo + NS-slot weight ring, persistent,
-  // weights pre-packed in step order per row tile (a different K order: chunk32-major, tap-minor)
-  CFG_RING_R128 = 27, CFG_RING_R64 = 28, CFG_RING_R128_NS3 = 29, CFG_RING_R64_NS5 = 30,
-  // 64-row ring stepping one kernel row (3 taps, 48 MFMAs per wave) per barrier, 3 slots of 3 taps
-  CFG_RING_R64_T3 = 31,
-  // ConvTranspose only: persistent ring GEMM, A and B through one 3-slot LDS-DMA ring (64-byte K steps)
-  CFG_TRING_R128 = 32,
-  // down1.0 fused into down1.3 on the 3-taps-per-step ring (halo chunks computed from the input)
-  CFG_RING_FUSED_IN = 33,
-  // ConvTranspose ring with the row tiles of one pixel tile taken back to back by one walker
-  CFG_TRING_R128_CTI = 34,
-  // ConvTranspose ring with 8-wave 256-row x 256-pixel block tiles (one block per CU)
-  CFG_TRING_R256 = 35, CFG_TRING_R256_NS4 = 36,
-  CFG_COUNT = 37
+  CFG_HALO_R64_W4 = 0,    // 64 rows x 16x16 pixels, 4 waves, 3 weight slots
+  CFG_HALO_R64_W8 = 1,    // 64 rows, 8 waves
+  CFG_HALO_R128 = 2,      // 128-row x 64-pixel wave tiles, 4 waves, 2 weight slots (also the fp32 ConvTranspose)
+  CFG_RING_R128 = 3,      // ring: 128-row x 64-pixel wave tiles, 3 weight slots, one tap per step
+  CFG_RING_R64_T3 = 4,    // ring: 64-row wave tiles, one kernel row (3 taps) per step
+  CFG_RING_FUSED_IN = 5,  // RING_R64_T3 for down1.3 with down1.0 fused (halo chunks computed from the input)
+  CFG_TRING_R128 = 6,     // ConvTranspose ring: 128-row x 256-pixel block tiles, 3 slots
+  CFG_TRING_R256 = 7,     // ConvTranspose ring: 8 waves, 256-row x 256-pixel block tiles, 4 slots
+  CFG_COUNT = 8
 };
-bool cfg_single_chunk(int cfg);
 int cfg_rows(int cfg);
-int cfg_pixels(int cfg);
 bool cfg_is_halo(int cfg);
 bool cfg_is_ring(int cfg);   // 64-byte-row ring kernel: step-major packed weights
 int ring_ns(int cfg);       // ring kernel: weight-ring slots
 int ring_tps(int cfg);      // ring kernel: taps per step
 bool cfg_is_tring(int cfg); // ConvTranspose ring kernel: step-major packed weights
-int cfg_limit();   // number of valid Cfg values in this build
 
-hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s);
+// t: operand (activation + weight) type; to / tq: types of the output / pooled map (t unless
+// the layer sits at a seam of the mixed bf16/fp16 plan)
+hipError_t launch_igemm(DType t, DType to, DType tq, int cfg, int taps, int epi, const IgemmArgs& a,
+                        hipStream_t s);
 hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s);
-// fp32 NCHW input -> T [N][H][W][4] (input of the fused first conv of CFG_RING_FUSED_IN)
-hipError_t launch_x_to_px4(DType t, const float* x, int N, int C, int H, int W, void* out, hipStream_t s);
+// Network input (fp32 or uint8 = value/255, NCHW or NHWC; include/unet_mi355x.h) -> element type
+// t, 4 channels per pixel [N][H][W][4] (input of the fused first conv of CFG_RING_FUSED_IN)
+hipError_t launch_x_to_px4(DType t, const void* x, int layout, int xdt, int N, int C, int H, int W, void* out,
+                           hipStream_t s);
+// the same input -> fp32 NCHW (the fp32 path's first conv reads fp32 NCHW)
+hipError_t launch_x_to_nchw_f32(const void* x, int layout, int xdt, int N, int C, int H, int W, float* out,
+                                hipStream_t s);
 // NHWC (pixel stride ld, channel offset choff, C channels) element type t -> NCHW fp32
 hipError_t launch_nhwc_to_nchw_f32(DType t, const void* src, int N, int H, int W, int C, int ld,
                                    int choff, float* dst, hipStream_t s);

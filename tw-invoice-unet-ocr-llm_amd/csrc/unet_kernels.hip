@@ -21,6 +21,8 @@
 //    zero-copy: producers write straight into channel halves of one NHWC buffer.
 #include "unet_internal.h"
 
+#include <type_traits>
+
 namespace unet {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -30,38 +32,17 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef int frag_t __attribute__((ext_vector_type(4)));   // one 16-byte MFMA operand fragment
 
 int cfg_rows(int cfg) {
-#ifdef UNET_ABLATION
-  if (cfg >= CFG_COUNT)
-    return (cfg == CFG_COUNT + 2 || cfg == CFG_COUNT + 3 || cfg == CFG_COUNT + 9 || cfg >= CFG_COUNT + 11) ? 128 : 64;
-#endif
-  return (cfg == CFG_R128_P128 || cfg == CFG_R128_P256 || cfg == CFG_HALO_R128_W4 || cfg == CFG_HALO_R128_W8 ||
-          cfg == CFG_HALO1_R128_W4 || cfg == CFG_PHALO_R128_W8 || cfg == CFG_HALO1_R128T8_NS2 ||
-          cfg == CFG_HALO1_R128T8_NS3 || cfg == CFG_SG_R128T8_NS2 || cfg == CFG_SG_R128T8_NS3 ||
-          cfg == CFG_RING_R128 || cfg == CFG_RING_R128_NS3 || cfg == CFG_TRING_R128 ||
-          cfg == CFG_TRING_R128_CTI) ? 128 : (cfg == CFG_TRING_R256 || cfg == CFG_TRING_R256_NS4 ? 256 : 64);
+  switch (cfg) {
+    case CFG_HALO_R128: case CFG_RING_R128: case CFG_TRING_R128: return 128;
+    case CFG_TRING_R256: return 256;
+    default: return 64;
+  }
 }
-bool cfg_single_chunk(int cfg) { (void)cfg; return false; }
-int cfg_pixels(int cfg) {
-  return (cfg == CFG_R64_P128 || cfg == CFG_R128_P128 || cfg == CFG_T8_HALO1_R64_W4 || cfg == CFG_T8_HALO_R64_W4 ||
-          cfg == CFG_T8_HALO_R64_W2) ? 128 : 256;
-}
-bool cfg_is_halo(int cfg) { return cfg >= CFG_HALO_R128_W4; }
-bool cfg_is_ring(int cfg) { return (cfg >= CFG_RING_R128 && cfg <= CFG_RING_R64_T3) || cfg == CFG_RING_FUSED_IN; }
-int ring_ns(int cfg) {
-  return (cfg == CFG_RING_R128_NS3 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN) ? 3
-                                                                                         : (cfg == CFG_RING_R64_NS5 ? 5 : 4);
-}
+bool cfg_is_halo(int cfg) { return cfg == CFG_HALO_R64_W4 || cfg == CFG_HALO_R64_W8 || cfg == CFG_HALO_R128; }
+bool cfg_is_ring(int cfg) { return cfg == CFG_RING_R128 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN; }
+int ring_ns(int cfg) { (void)cfg; return 3; }
 int ring_tps(int cfg) { return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN) ? 3 : 1; }
-bool cfg_is_tring(int cfg) {
-  return cfg == CFG_TRING_R128 || cfg == CFG_TRING_R128_CTI || cfg == CFG_TRING_R256 || cfg == CFG_TRING_R256_NS4;
-}
-int cfg_limit() {
-#ifdef UNET_ABLATION
-  return CFG_COUNT + 15;
-#else
-  return CFG_COUNT;
-#endif
-}
+bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128 || cfg == CFG_TRING_R256; }
 
 // ---------------------------------------------------------------------------------
 // element traits
@@ -96,6 +77,11 @@ __device__ __forceinline__ void mfma_frag<float>(f32x4& acc, const uint4& a, con
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], acc, 0, 0, 0);
 }
+
+// torch semantics of ReLU / MaxPool2d: a NaN propagates (unet_model.py:12,16,34).  One
+// v_maximum3_f32 (IEEE-754-2019 maximum) each; fmaxf would turn a NaN into the other operand.
+__device__ __forceinline__ float relu_nan(float x) { return __builtin_elementwise_maximum(x, 0.f); }
+__device__ __forceinline__ float max_nan(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 
 // store 16 consecutive channels (fp32 values) as element type T (16-byte vector stores)
 template <typename T>
@@ -177,7 +163,9 @@ __device__ __forceinline__ float xsum_lane32(float x) {   // x[l] + x[l ^ 32]
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-template <typename T, int TP, int EPI>
+// TO: element type of the NHWC output (and of the ConvTranspose scatter), TQ: of the pooled map
+// (the two differ where a layer feeds consumers of different storage type, see unet_capi.cpp).
+template <typename TO, typename TQ, int TP, int EPI>
 __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0,
                                               int ox0, int g0, int row0, const float* bias_w,
                                               const float* head_w, const float* head_b) {
@@ -208,13 +196,13 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float x = acc[t][p][e] + bv[t * 4 + e];
-        if (EPI != EPI_UPSCATTER) x = fmaxf(x, 0.f);
+        if (EPI != EPI_UPSCATTER) x = relu_nan(x);
         v[t * 4 + e] = x;
       }
     if constexpr (EPI == EPI_STORE || EPI == EPI_POOL) {
       if (inside) {
-        T* dst = reinterpret_cast<T*>(a.out) + ((long long)(n * H + oy) * W + ox) * a.ldo + a.out_off + rbase;
-        store16<T>(dst, v);
+        TO* dst = reinterpret_cast<TO*>(a.out) + ((long long)(n * H + oy) * W + ox) * a.ldo + a.out_off + rbase;
+        store16<TO>(dst, v);
       }
       if constexpr (EPI == EPI_POOL) {
         float m[16];
@@ -222,14 +210,14 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
         for (int e = 0; e < 16; ++e) {
           // 2x2 window partners are lanes ^1 (quad_perm [1,0,3,2]) and ^8 (row_ror:8):
           // DPP moves instead of ds_bpermute round trips through LDS.
-          const float o = fmaxf(v[e], dpp_f32<0xB1>(v[e]));
-          m[e] = fmaxf(o, dpp_f32<0x128>(o));
+          const float o = max_nan(v[e], dpp_f32<0xB1>(v[e]));
+          m[e] = max_nan(o, dpp_f32<0x128>(o));
         }
         if ((col & 9) == 0 && oy + 1 < H && ox + 1 < W) {
           const int Ho = H >> 1, Wo = W >> 1;
-          T* dst = reinterpret_cast<T*>(a.out2) +
-                   ((long long)(n * Ho + (oy >> 1)) * Wo + (ox >> 1)) * a.ldo2 + rbase;
-          store16<T>(dst, m);
+          TQ* dst = reinterpret_cast<TQ*>(a.out2) +
+                    ((long long)(n * Ho + (oy >> 1)) * Wo + (ox >> 1)) * a.ldo2 + rbase;
+          store16<TQ>(dst, m);
         }
       }
     } else if constexpr (EPI == EPI_UPSCATTER) {
@@ -237,9 +225,9 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
         const int ab = rbase / a.Cout;
         const int o0 = rbase - ab * a.Cout;
         const int Y = 2 * oy + (ab >> 1), X = 2 * ox + (ab & 1);
-        T* dst = reinterpret_cast<T*>(a.out) +
-                 ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0;
-        store16<T>(dst, v);
+        TO* dst = reinterpret_cast<TO*>(a.out) +
+                  ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0;
+        store16<TO>(dst, v);
       }
     } else {  // EPI_HEAD: 1x1 conv 64 -> ncls on the fp32 activations, then masks
       // All class dots first (independent FMA chains), then the 4 row-quads of the
@@ -284,146 +272,22 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
 
 
 // ---------------------------------------------------------------------------------
-// implicit-GEMM kernel
+// 3x3 conv with an LDS halo tile (the fp32 path; 128-byte K chunks)
 // ---------------------------------------------------------------------------------
-// WR waves along rows (64 rows each, 4 MFMA row tiles), WPX waves along pixels
-// (TP MFMA column tiles of 16 pixels each).  4 waves per block.
-template <typename T, int WR, int WPX, int TP, int TAPS, int EPI>
-__global__ __launch_bounds__(256, 2) void igemm_kernel(const IgemmArgs a) {
-  static_assert(WR * WPX == 4, "4 waves per block");
-  constexpr int TC = 4;
-  constexpr int BR = WR * 64;
-  constexpr int BP = WPX * TP * 16;
-  constexpr int TH = BP / 16;
-  constexpr int BKE = Elem<T>::BKE;
-  constexpr int STAGE = (BR + BP) * 128;
-  constexpr int A_INS = BR / 32;  // glds instructions per wave for the A tile
-  constexpr int B_INS = BP / 32;  // ... for the B tile
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
-
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int lane = tid & 63;
-  const int wr = wave / WPX;
-  const int wp = wave % WPX;
-
-  // XCD-aware bijective remap: hardware deals blocks round-robin over 8 XCDs; give each
-  // XCD a contiguous range so that the n_ct row tiles of one pixel tile (which share the
-  // gathered activations) run on one L2.
-  int lid;
-  {
-    const int nb = a.n_blocks, q = nb >> 3, r = nb & 7;
-    const int bid = blockIdx.x, x = bid & 7, k = bid >> 3;
-    lid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-  }
-  const int ct = lid % a.n_ct;
-  int mt = lid / a.n_ct;
-  const int tx = mt % a.tiles_x;
-  mt /= a.tiles_x;
-  const int ty = mt % a.tiles_y;
-  const int n = mt / a.tiles_y;
-
-  const int H = a.H, W = a.W;
-  const int K = TAPS * a.Cin;
-  const int cpt = a.Cin / BKE;  // 128-byte chunks per tap
-  const int S = TAPS * cpt;
-
-  // per-lane source chunk (XOR swizzle through the source address; LDS stays lane-linear)
-  const int src_chunk = (lane & 7) ^ ((lane >> 3) & 7);
-  const char* zero = reinterpret_cast<const char*>(a.zero) + src_chunk * 16;
-
-  // B rows owned by this lane: (oy, ox) of the output pixel and its flattened index
-  int b_oy[B_INS], b_ox[B_INS], b_pix[B_INS];
-#pragma unroll
-  for (int j = 0; j < B_INS; ++j) {
-    const int row = wave * (BP / 4) + j * 8 + (lane >> 3);
-    int py, px;
-    pix_of(row, py, px);
-    b_oy[j] = ty * TH + py;
-    b_ox[j] = tx * 16 + px;
-    b_pix[j] = (n * H + b_oy[j]) * W + b_ox[j];
-  }
-  const char* wsrc[A_INS];
-#pragma unroll
-  for (int j = 0; j < A_INS; ++j) {
-    const int row = wave * (BR / 4) + j * 8 + (lane >> 3);
-    wsrc[j] = reinterpret_cast<const char*>(a.wgt) +
-              ((size_t)(ct * BR + row) * K) * sizeof(T) + src_chunk * 16;
-  }
-  const char* in = reinterpret_cast<const char*>(a.in) + src_chunk * 16;
-
-  auto stage = [&](int s, int buf) {
-    const int tap = s / cpt;
-    const int c0 = (s - tap * cpt) * BKE;
-    char* As = lds + buf * STAGE;
-    char* Bs = As + BR * 128;
-#pragma unroll
-    for (int j = 0; j < A_INS; ++j)
-      glds16(wsrc[j] + (size_t)s * BKE * sizeof(T), As + (wave * (BR / 4) + j * 8) * 128);
-    int dy = 0, dx = 0;
-    if (TAPS == 9) { dy = tap / 3 - 1; dx = tap - (tap / 3) * 3 - 1; }
-#pragma unroll
-    for (int j = 0; j < B_INS; ++j) {
-      const int iy = b_oy[j] + dy, ix = b_ox[j] + dx;
-      const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W &&
-                      b_oy[j] < H && b_ox[j] < W;
-      const char* src = ok ? in + ((long long)(b_pix[j] + dy * W + dx) * a.ldi + c0) * (long long)sizeof(T)
-                           : zero;
-      glds16(src, Bs + (wave * (BP / 4) + j * 8) * 128);
-    }
-  };
-
-  f32x4 acc[TC][TP];
-#pragma unroll
-  for (int t = 0; t < TC; ++t)
-#pragma unroll
-    for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const int frag_row = lane & 15;
-  for (int s = 0; s < S; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < S) stage(s + 1, buf ^ 1);
-    const char* As = lds + buf * STAGE + (wr * 64 + frag_row) * 128;
-    const char* Bs = lds + buf * STAGE + BR * 128 + (wp * TP * 16 + frag_row) * 128;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int phys = ((kk * 4 + (lane >> 4)) ^ (lane & 7)) * 16;
-      uint4 af[TC], bfv[TP];
-#pragma unroll
-      for (int t = 0; t < TC; ++t) af[t] = *reinterpret_cast<const uint4*>(As + t * 16 * 128 + phys);
-#pragma unroll
-      for (int p = 0; p < TP; ++p) bfv[p] = *reinterpret_cast<const uint4*>(Bs + p * 16 * 128 + phys);
-#pragma unroll
-      for (int t = 0; t < TC; ++t)
-#pragma unroll
-        for (int p = 0; p < TP; ++p) mfma_frag<T>(acc[t][p], af[t], bfv[p]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  conv_epilogue<T, TP, EPI>(a, acc, n, ty * TH, tx * 16, wp * TP, ct * BR + wr * 64,
-                            a.bias + ct * BR + wr * 64, a.head_w + wr * 64, a.head_b);
-}
-
-// ---------------------------------------------------------------------------------
-// 3x3 conv with an LDS halo tile (the main kernel for 3x3 layers)
-// ---------------------------------------------------------------------------------
-// Block = BR output channels x a 16x16 output-pixel tile.  Per 64-channel (128-byte) input
-// chunk the block stages the 18x18 input halo ONCE into LDS; the nine taps then read
-// shifted windows of it, so the activation operand is fetched from L2 once per chunk
-// instead of nine times.  Weights stream through a 3-slot ring, two K-steps ahead.  All
+// Block = BR output channels x a 16x16 output-pixel tile.  Per 128-byte input chunk (32 f32 /
+// 64 bf16 channels) the block stages the 18x18 input halo ONCE into LDS; the nine taps then
+// read shifted windows of it, so the activation operand is fetched from L2 once per chunk
+// instead of nine times.  Weights stream through an NS-slot ring, NS-1 K-steps ahead.  All
 // staging is LDS-DMA (global_load_lds_dwordx4) with counted vmcnt waits, so loads stay in
-// flight across the per-step barrier.
+// flight across the per-step barrier.  One halo buffer, two blocks per CU: the other block
+// covers this one's exposed halo load and epilogue.
 //
-// LDS: [halo 0][halo 1][w slot 0][w slot 1][w slot 2]; halo pixel (hy,hx) -> row hy*18+hx
+// LDS: [halo][w slot 0 .. NS-1][bias/head params]; halo pixel (hy,hx) -> row hy*18+hx
 // (128 B), 16-byte chunk c stored at c ^ (hx & 7): conflict-free ds_read_b128 for every tap
 // (the 18-pixel row stride breaks the usual row&7 swizzle).  Weight rows: c ^ (row & 7).
-constexpr int kHaloPix = 18 * 18;
+// KT = 3: 3x3 conv (18x18 halo, 9 taps); KT = 1: the same pipeline as a plain GEMM over a
+// 16x16 pixel tile (ConvTranspose2d k2 s2 on the fp32 path: K = Cin, rows = (a, b, cout),
+// EPI_UPSCATTER).
 constexpr int kNumCUs = 256;          // MI355X: 8 XCDs x 32 CUs
 
 // s_waitcnt vmcnt(N) lgkmcnt(0) + s_barrier.  The wait goes through the builtin (not asm) so
@@ -439,63 +303,37 @@ __device__ __forceinline__ void wait_vm_barrier() {
 }
 
 // Derived geometry / LDS budget of a halo-kernel instantiation (shared with the launcher).
-template <typename T, int WR, int WPX, int TCW, int HB, int NS, int HSRC, int KT, int TH>
+template <typename T, int WR, int WPX, int TCW, int NS, int KT>
 struct HaloGeom {
   static constexpr int NW = WR * WPX;
   static constexpr int TC = TCW;
-  static constexpr int TP = TH / WPX;               // 16-pixel groups per wave (TH groups/tile)
+  static constexpr int TP = 16 / WPX;               // 16-pixel groups per wave (16 per tile)
   static constexpr int BR = WR * 16 * TC;
   static constexpr int BKE = Elem<T>::BKE;
   static constexpr int PAD = KT == 3 ? 1 : 0;
-  static constexpr int HWD = 16 + 2 * PAD;          // halo width
-  static constexpr int HHT = TH + 2 * PAD;          // halo height
-  static constexpr int NPIX = HWD * HHT;
+  static constexpr int HWD = 16 + 2 * PAD;          // halo width = height
+  static constexpr int NPIX = HWD * HWD;
   static constexpr int NTAP = KT * KT;
-  // halo DMA is issued by the first HLW waves (all waves, except 4 of 8 for a 3-deep ring so
-  // the per-buffer padding stays small): HI instructions (8 pixel rows each) per loader wave
-  static constexpr int HLW = (HB == 3 && NW > 4) ? 4 : NW;
-  static constexpr int HI = (NPIX + 8 * HLW - 1) / (8 * HLW);
-  static constexpr int HROWS = HI * HLW * 8;
-  static constexpr int WI = BR / (8 * NW);
-  static constexpr int HALO_BYTES = HROWS * 128;
+  static constexpr int HI = (NPIX + 8 * NW - 1) / (8 * NW);   // halo DMA instructions per wave
+  static constexpr int WI = BR / (8 * NW);                     // weight DMA instructions per wave
+  static constexpr int HALO_BYTES = HI * NW * 8 * 128;
   static constexpr int WSLOT = BR * 128;
-  static constexpr int WOFF = HB * HALO_BYTES;
+  static constexpr int WOFF = HALO_BYTES;
   static constexpr int PARAM_OFF = WOFF + NS * WSLOT;
-  static constexpr int XS_OFF = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
-  static constexpr int XSW = 20, XSH = TH + 4;       // fused input window (HSRC = 1)
-  static constexpr int XS_FLOATS = HSRC ? 3 * XSW * XSH : 0;
-  static constexpr int LDS_BYTES = XS_OFF + XS_FLOATS * 4;
-  static constexpr int BLOCKS_PER_CU = (160 * 1024) / LDS_BYTES;
+  static constexpr int LDS_BYTES = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
 };
 
-template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int HSRC, int KT, int TH, int EPI>
-__global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void conv3x3_halo_kernel(const IgemmArgs a) {
-  // HB = 2 (persistent): gridDim.x = n_ct * n_slots blocks (host), each with a fixed row
-  // tile ct, walks pixel tiles mt = slot, slot + n_slots, ...  The K-step pipeline (halo of
-  // the next chunk, weights two steps ahead) runs continuously across tile boundaries, so
-  // the next tile's loads overlap this tile's last steps and epilogue.
-  // HB = 1: one halo buffer, one tile per block; the next chunk's halo is loaded after the
-  // last tap of the current one (an exposed load per chunk), but the block is small enough
-  // for two blocks per CU, which then cover each other's halo loads and epilogues.
-  // NS = weight-ring slots; weights are prefetched NS-1 steps ahead.
-  // TCW = 16-row MFMA tiles per wave (4: 64 rows, 8: 128 rows = two 64-row epilogue groups).
-  // HSRC = 1: the layer is down1.3 and its input (down1.0's output) is never materialised:
-  // the 18x18x64 halo is computed in the prologue from the raw fp32 input (first conv on
-  // MFMA, K = 9*C padded to 32), which removes a 32 MB/image write + read.
-  // KT = 3: 3x3 conv ((TH+2)x18 halo, 9 taps); KT = 1: the same pipeline as a plain GEMM over a
-  // THx16 pixel tile (ConvTranspose2d k2 s2: K = Cin, rows = (a, b, cout), EPI_UPSCATTER).
-  // TH = pixel-tile height (16, or 8 for a smaller LDS footprint and more blocks per CU).
-  using G = HaloGeom<T, WR, WPX, TCW, HB, NS, HSRC, KT, TH>;
+template <typename T, int WR, int WPX, int TCW, int NS, int KT, int EPI>
+__global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_kernel(const IgemmArgs a) {
+  using G = HaloGeom<T, WR, WPX, TCW, NS, KT>;
   constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
   constexpr int HWD = G::HWD, NPIX = G::NPIX, NTAP = G::NTAP, PAD = G::PAD;
-  constexpr int HI = G::HI, WI = G::WI, HALO_BYTES = G::HALO_BYTES, WSLOT = G::WSLOT, HLW = G::HLW;
-  constexpr int WOFF = G::WOFF, PARAM_OFF = G::PARAM_OFF, XS_OFF = G::XS_OFF;
-  constexpr int XSW = G::XSW, XSH = G::XSH;
-  static_assert(TP >= 1 && TH % WPX == 0, "pixel groups per wave");
+  constexpr int HI = G::HI, WI = G::WI, WSLOT = G::WSLOT, WOFF = G::WOFF;
+  static_assert(NS == 2 || NS == 3, "weight ring depth");
   static_assert(WI >= 1 && BR % (8 * NW) == 0, "weight tile split");
-  static_assert(HSRC == 0 || (HB == 1 && sizeof(T) == 2 && KT == 3), "fused input halo: 3x3, single buffer, 16-bit");
+  static_assert(G::LDS_BYTES <= 160 * 1024 / 2, "two blocks per CU");
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
-  float* bias_s = reinterpret_cast<float*>(lds + PARAM_OFF);
+  float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
   float* headw_s = bias_s + BR;
   float* headb_s = headw_s + kMaxClasses * 64;
 
@@ -504,14 +342,6 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   const int lane = tid & 63;
   const int wr = wave / WPX;
   const int wp = wave % WPX;
-  // PIPE 6 (diagnostic build only): s_memtime stamps -> per-wave cycle breakdown in a.dbg
-  constexpr bool kStamp = PIPE == 6;
-  auto stamp = [&]() -> unsigned long long {
-    unsigned long long t = 0;
-    if constexpr (kStamp) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
-    return t;
-  };
-  unsigned long long st_t0 = stamp(), st_pro = 0, st_cmp = 0, st_wait = 0, st_epi = 0, st_steps = 0;
 
   int bid;
   {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one pixel tile
@@ -520,59 +350,34 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
   }
   const int ct = bid % a.n_ct;
-  const int slot = bid / a.n_ct;
-  const int n_slots = gridDim.x / a.n_ct;
-  const int n_mt = a.N * a.tiles_y * a.tiles_x;
-  if (slot >= n_mt) return;
-  const int items = (n_mt - slot + n_slots - 1) / n_slots;
+  int mt = bid / a.n_ct;
+  const int tx = mt % a.tiles_x;
+  mt /= a.tiles_x;
+  const int ty = mt % a.tiles_y;
+  const int n = mt / a.tiles_y;
+  if (n >= a.N) return;
 
   const int H = a.H, W = a.W;
   const int K = NTAP * a.Cin;
   const int nch = a.Cin / BKE;
   const int S = NTAP * nch;
-  const int total = items * S;
-  const int hseq_end = items * nch;
 
-  // per-block epilogue parameters into LDS with plain loads, issued after the first DMAs so
-  // the two latencies overlap (their vmcnt(0) also covers the DMAs; the prologue's barrier
-  // publishes them)
-  auto load_params = [&]() {
-    for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];
-    if (EPI == EPI_HEAD) {
-      for (int i = tid; i < a.ncls * 64; i += 64 * NW) headw_s[i] = a.head_w[i];
-      if (tid < a.ncls) headb_s[tid] = a.head_b[tid];
-    }
-  };
-
-  // Halo rows owned by this lane are recomputed at every (once-per-chunk) halo issue
-  // instead of being kept in ~3*HI registers; weight rows: one base pointer per lane.
   const int w_chk = ((lane & 7) ^ ((lane >> 3) & 7)) * 16;
   const char* wbase = reinterpret_cast<const char*>(a.wgt) +
                       (size_t)(ct * BR + wave * WI * 8 + (lane >> 3)) * K * sizeof(T) + w_chk;
   const size_t wstep = (size_t)8 * K * sizeof(T);   // 8 rows per DMA instruction
   const char* in = reinterpret_cast<const char*>(a.in);
   const char* zero = reinterpret_cast<const char*>(a.zero);
+  const long long pix0 = (long long)(n * H + ty * 16) * W + tx * 16;
 
-  auto tile_of = [&](int i, int& n, int& ty, int& tx) {
-    int mt = slot + i * n_slots;
-    tx = mt % a.tiles_x;
-    mt /= a.tiles_x;
-    ty = mt % a.tiles_y;
-    n = mt / a.tiles_y;
-  };
-  auto issue_halo = [&](int hseq) {
-    const int i = hseq / nch, c = hseq - (hseq / nch) * nch;
-    int n, ty, tx;
-    tile_of(i, n, ty, tx);
-    if (wave >= HLW) return;   // (wave-uniform) not a halo loader
-    char* dst = lds + (hseq % HB) * HALO_BYTES + wave * HI * 8 * 128;
+  auto issue_halo = [&](int c) {
+    char* dst = lds + wave * HI * 8 * 128;
     const long long c0 = (long long)c * BKE;
-    const long long pix0 = (long long)(n * H + ty * TH) * W + tx * 16;
 #pragma unroll
     for (int j = 0; j < HI; ++j) {
       const int row = (wave * HI + j) * 8 + (lane >> 3);
       const int hy = row / HWD, hx = row - hy * HWD;
-      const int iy = ty * TH + hy - PAD, ix = tx * 16 + hx - PAD;
+      const int iy = ty * 16 + hy - PAD, ix = tx * 16 + hx - PAD;
       const bool ok = row < NPIX && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       const int chk = ((lane & 7) ^ (hx & 7)) * 16;
       const long long pix = pix0 + (long long)(hy - PAD) * W + (hx - PAD);
@@ -580,9 +385,8 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
       glds16(src, dst + j * 8 * 128);
     }
   };
-  auto issue_w = [&](int g) {
-    const int s = g % S;
-    const int c = s / NTAP, tap = s - (s / NTAP) * NTAP;
+  auto issue_w = [&](int g) {   // K step g = (chunk, tap), weights [row][tap*Cin + c]
+    const int c = g / NTAP, tap = g - (g / NTAP) * NTAP;
     const size_t koff = ((size_t)tap * a.Cin + (size_t)c * BKE) * sizeof(T);
     char* dst = lds + WOFF + (g % NS) * WSLOT + wave * WI * 8 * 128;
 #pragma unroll
@@ -605,92 +409,20 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
   }
   const int px_lane = col & 7;
 
-  if constexpr (HSRC == 1) {
-    issue_w(0);
-    if (NS == 3 && total > 1) issue_w(1);
-    load_params();
-    // --- fused down1.0: raw input window 20x20xC -> first conv on MFMA -> LDS halo ---
-    float* xs = reinterpret_cast<float*>(lds + XS_OFF);
-    int n0, ty0, tx0;
-    tile_of(0, n0, ty0, tx0);
-    const int C0 = a.c0;
-    for (int i = tid; i < C0 * XSW * XSH; i += 64 * NW) {
-      const int c = i / (XSW * XSH), r = i - c * (XSW * XSH), yy = r / XSW, xx = r - (r / XSW) * XSW;
-      const int iy = ty0 * TH + yy - 2, ix = tx0 * 16 + xx - 2;
-      const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      xs[i] = ok ? static_cast<const float*>(a.x0)[(((long long)n0 * C0 + c) * H + iy) * W + ix] : 0.f;
-    }
-    frag_t wf[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-      wf[t] = *reinterpret_cast<const frag_t*>(reinterpret_cast<const char*>(a.w0p) +
-                                               ((t * 16 + (lane & 15)) * 32 + 8 * (lane >> 4)) * sizeof(T));
-    float b0v[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) b0v[e] = a.b0[(lane >> 4) * 16 + e];
-    int koff[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * (lane >> 4) + j;
-      const int c = k / 9, r = k - (k / 9) * 9;
-      koff[j] = k < 9 * C0 ? c * (XSW * XSH) + (r / 3) * XSW + (r - (r / 3) * 3) : -1;
-    }
-    __syncthreads();
-    for (int grp = wave; grp * 16 < NPIX; grp += NW) {
-      const int p = grp * 16 + (lane & 15);
-      const bool real = p < NPIX;
-      const int hy = real ? p / 18 : 0, hx = real ? p - (p / 18) * 18 : 0;
-      typedef T t8 __attribute__((ext_vector_type(8)));
-      t8 hv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) hv[j] = (T)(koff[j] >= 0 ? xs[koff[j] + hy * XSW + hx] : 0.f);
-      const uint4 bfr = __builtin_bit_cast(uint4, hv);
-      f32x4 acc0[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        mfma_frag<T>(acc0[t], __builtin_bit_cast(uint4, wf[t]), bfr);
-      }
-      // zero outside the image: these are down1.3's conv padding, not relu(bias)
-      const int iy = ty0 * TH + hy - 1, ix = tx0 * 16 + hx - 1;
-      const bool inimg = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      t8 lo, hi;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float v = inimg ? fmaxf(acc0[t][e] + b0v[t * 4 + e], 0.f) : 0.f;
-          if (t < 2) lo[t * 4 + e] = (T)v; else hi[(t - 2) * 4 + e] = (T)v;
-        }
-      if (real) {
-        const int q = lane >> 4;
-        char* row = lds + p * 128;
-        *reinterpret_cast<uint4*>(row + (((2 * q) ^ (hx & 7)) << 4)) = __builtin_bit_cast(uint4, lo);
-        *reinterpret_cast<uint4*>(row + (((2 * q + 1) ^ (hx & 7)) << 4)) = __builtin_bit_cast(uint4, hi);
-      }
-    }
-    if (NS == 3 && total > 1) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
-  } else {
   issue_halo(0);
   issue_w(0);
-  if (HB == 3 && hseq_end > 1) issue_halo(1);   // 3-deep ring: two chunks ahead from the start
-  if (NS == 3 && total > 1) issue_w(1);
-  load_params();
-  if (NS == 3 && total > 1) {
-    if (HB == 3 && hseq_end > 1) {
-      if (wave < HLW) wait_vm_barrier<HI + WI>(); else wait_vm_barrier<WI>();
-    } else {
-      wait_vm_barrier<WI>();
-    }
-  } else {
-    if (HB == 3 && hseq_end > 1 && wave < HLW) wait_vm_barrier<HI>(); else wait_vm_barrier<0>();
+  if (NS == 3 && S > 1) issue_w(1);
+  // epilogue parameters into LDS with plain loads, issued after the first DMAs so the two
+  // latencies overlap (their vmcnt(0) also covers the DMAs; the barrier publishes them)
+  for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];
+  if (EPI == EPI_HEAD) {
+    for (int i = tid; i < a.ncls * 64; i += 64 * NW) headw_s[i] = a.head_w[i];
+    if (tid < a.ncls) headb_s[tid] = a.head_b[tid];
   }
-  }
+  if (NS == 3 && S > 1) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
 
-  // fragment reads of (step, kk) into a register set
-  auto read_frags = [&](int g, int hs, int tp, int kk, frag_t (&af)[TC], frag_t (&bf)[TP]) {
+  auto read_frags = [&](int g, int tp, int kk, frag_t (&af)[TC], frag_t (&bf)[TP]) {
     const int dy = tp / KT, dx = tp - (tp / KT) * KT;
-    const char* Hs = lds + (hs % HB) * HALO_BYTES;
     const char* Ws = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 128;
     const int toff = dy * HWD + dx;
     const int hx7 = (px_lane + dx) & 7;
@@ -700,166 +432,45 @@ __global__ __launch_bounds__(64 * WR * WPX, HB == 1 ? 2 * WR * WPX / 4 : 1) void
       af[t] = *reinterpret_cast<const frag_t*>(Ws + t * 16 * 128 + ((chunk ^ (lane & 7)) << 4));
 #pragma unroll
     for (int p = 0; p < TP; ++p)
-      bf[p] = *reinterpret_cast<const frag_t*>(Hs + (prow[p] + toff) * 128 + ((chunk ^ hx7) << 4));
+      bf[p] = *reinterpret_cast<const frag_t*>(lds + (prow[p] + toff) * 128 + ((chunk ^ hx7) << 4));
   };
   auto mfmas = [&](const frag_t (&af)[TC], const frag_t (&bf)[TP]) {
 #pragma unroll
     for (int t = 0; t < TC; ++t)
 #pragma unroll
       for (int p = 0; p < TP; ++p)
-        if constexpr (PIPE == 2) asm volatile("" ::"v"(af[t]), "v"(bf[p]));   // ablation: no MFMA
-        else mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af[t]), __builtin_bit_cast(uint4, bf[p]));
-  };
-  // after the barrier (which retired every LDS read with lgkmcnt(0)), declare the kk=1
-  // fragments "re-defined" so hipcc does not re-wait for their reads behind the next
-  // step's kk=0 reads (its waitcnt tracker does not model the barrier's wait)
-  auto reg_fence = [&](frag_t (&af)[TC], frag_t (&bf)[TP]) {
-#pragma unroll
-    for (int t = 0; t < TC; ++t) asm volatile("" : "+v"(af[t]) : : "memory");
-#pragma unroll
-    for (int p = 0; p < TP; ++p) asm volatile("" : "+v"(bf[p]) : : "memory");
-  };
-  // PIPE 7: one step as a fixed read/MFMA interleave.  The A (weight) fragments stream
-  // through a 3-register ring, each read two MFMA groups ahead of its use; the B (halo)
-  // fragments of kk = 1 are read during the kk = 0 groups.  sched_group_barrier pins the
-  // order, so the waits in front of each MFMA group cover only reads issued >= 2 groups
-  // earlier (hipcc's default schedule under register pressure reuses ONE A register and
-  // waits lgkmcnt(0) in front of every group).
-  auto step_sg = [&](int g, int hs, int tp) {
-    const int dy = tp / KT, dx = tp - (tp / KT) * KT;
-    const char* Hs = lds + (hs % HB) * HALO_BYTES;
-    const char* Ws = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 128;
-    const int toff = dy * HWD + dx;
-    const int hx7 = (px_lane + dx) & 7;
-    const int l7 = lane & 7;
-    constexpr int NI = 2 * TC;
-    frag_t bq[2][TP], ar[3];
-    auto rdA = [&](int i) {
-      const int kk = i / TC, t = i - (i / TC) * TC;
-      return *reinterpret_cast<const frag_t*>(Ws + t * 16 * 128 + (((kk * 4 + q) ^ l7) << 4));
-    };
-    auto rdB = [&](int kk, int p) {
-      return *reinterpret_cast<const frag_t*>(Hs + (prow[p] + toff) * 128 + (((kk * 4 + q) ^ hx7) << 4));
-    };
-#pragma unroll
-    for (int p = 0; p < TP; ++p) bq[0][p] = rdB(0, p);
-    ar[0] = rdA(0);
-    ar[1] = rdA(1);
-    __builtin_amdgcn_sched_group_barrier(0x100, TP + 2, 0);
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      int nr = 0;
-      if (i + 2 < NI) { ar[(i + 2) % 3] = rdA(i + 2); ++nr; }
-      if (i >= 1 && i <= TP) { bq[1][i - 1] = rdB(1, i - 1); ++nr; }
-      const frag_t a = ar[i % 3];
-#pragma unroll
-      for (int p = 0; p < TP; ++p)
-        mfma_frag<T>(acc[i % TC][p], __builtin_bit_cast(uint4, a), __builtin_bit_cast(uint4, bq[i / TC][p]));
-      if (nr == 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // i is unrolled: nr folds
-      else if (nr == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
-    }
+        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af[t]), __builtin_bit_cast(uint4, bf[p]));
   };
 
   frag_t a0[TC], b0[TP], a1[TC], b1[TP];
-  if (PIPE == 1 || PIPE == 5) read_frags(0, 0, 0, 0, a0, b0);
-
-  int c = 0, tap = 0, hseq = 0, item = 0;
-  if constexpr (kStamp) st_pro = stamp() - st_t0;
-  for (int g = 0; g < total; ++g) {
-    const unsigned long long st_a = stamp();
-    // ring of HB halo buffers: at a chunk's first tap, prefetch the halo HB-1 chunks ahead
-    const bool hnext = HB >= 2 && (tap == 0) && (hseq + HB - 1 < hseq_end);
-    const bool wnext = g + NS - 1 < total;
-    constexpr bool kDma = PIPE < 3 || PIPE > 5;   // ablations 3, 4, 5: no DMA in the loop
-    constexpr bool kDmaW = kDma && PIPE != 8;     // ablation 8: halo DMA only
-    constexpr bool kDmaH = kDma && PIPE != 9;     // ablation 9: weight DMA only
-    constexpr bool kPipe = PIPE == 1 || PIPE == 5;
-    if (kDmaH && hnext) issue_halo(hseq + HB - 1);
-    if (kDmaW && wnext) issue_w(g + NS - 1);
-
-    if constexpr (PIPE == 7) {
-      step_sg(g, hseq, tap);
-    } else if (kPipe) {
-      // kk=1 reads in flight behind the kk=0 MFMAs; kk=0 of the next step is read right
-      // after the barrier, behind this step's kk=1 MFMAs: no read-latency bubble per step.
-      read_frags(g, hseq, tap, 1, a1, b1);
-      mfmas(a0, b0);
-    } else {
-      read_frags(g, hseq, tap, 0, a0, b0);
-      mfmas(a0, b0);
-      // 128-row wave tiles: keep one kk's fragments live at a time (register budget)
-      if constexpr (TC == 8) __builtin_amdgcn_sched_barrier(0);
-      read_frags(g, hseq, tap, 1, a1, b1);
-      mfmas(a1, b1);
-    }
-    // the next step needs W(g+1) and, at a chunk end, the next halo.  That halo was issued
-    // (HB-1)*NTAP steps earlier; it is older than this step's loads except when it was issued
-    // in THIS step (HB = 2 ring over a single-tap GEMM, KT = 1), where the wait must cover it.
-    // The barrier's lgkmcnt(0) also retires every fragment read of this step (WAR).
-    constexpr bool kHaloNextStep = (HB - 1) * NTAP == 1;
-    const unsigned long long st_b = stamp();
-    if (PIPE == 4) {
-      // ablation: no barrier
-    } else if (NS == 2) {
+  int c = 0, tap = 0;
+  for (int g = 0; g < S; ++g) {
+    const bool wnext = g + NS - 1 < S;
+    if (wnext) issue_w(g + NS - 1);
+    read_frags(g, tap, 0, a0, b0);
+    mfmas(a0, b0);
+    // 128-row wave tiles: keep one kk's fragments live at a time (register budget)
+    if constexpr (TC == 8) __builtin_amdgcn_sched_barrier(0);
+    read_frags(g, tap, 1, a1, b1);
+    mfmas(a1, b1);
+    // the next step needs W(g+1); the barrier's lgkmcnt(0) also retires this step's reads (WAR)
+    if (NS == 2) {
       wait_vm_barrier<0>();
-    } else if (hnext && wave < HLW && !kHaloNextStep) {
-      if (wnext) wait_vm_barrier<HI + WI>(); else wait_vm_barrier<HI>();
     } else {
       if (wnext) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
     }
-    if (HB == 1 && tap == NTAP - 1 && hseq + 1 < hseq_end) {
-      if (kDmaH) issue_halo(hseq + 1);   // every wave has finished reading the halo (barrier above)
+    if (tap == NTAP - 1 && c + 1 < nch) {   // every wave has finished reading the halo (barrier above)
+      issue_halo(c + 1);
       wait_vm_barrier<0>();
     }
-
-    if constexpr (kStamp) {
-      const unsigned long long st_c = stamp();
-      st_cmp += st_b - st_a;
-      st_wait += st_c - st_b;
-      ++st_steps;
-    }
-    bool tile_end = false;
-    if (++tap == NTAP) {
-      tap = 0;
-      ++hseq;
-      if (++c == nch) {
-        c = 0;
-        tile_end = true;
-      }
-    }
-    if (kPipe) {
-      reg_fence(a1, b1);
-      // unconditional (clamped) so there is no control-flow merge in front of the MFMAs:
-      // hipcc's waitcnt tracker would otherwise re-wait for this step's retired reads
-      read_frags(g + 1 < total ? g + 1 : g, hseq, tap, 0, a0, b0);
-      mfmas(a1, b1);
-    }
-    if (tile_end) {
-      const unsigned long long st_e = stamp();
-      int n, ty, tx;
-      tile_of(item, n, ty, tx);
-#pragma unroll
-      for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<T, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * TH, tx * 16,
-                                  wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h,
-                                  headw_s, headb_s);
-#pragma unroll
-      for (int t = 0; t < TC; ++t)
-#pragma unroll
-        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-      ++item;
-      if constexpr (kStamp) st_epi += stamp() - st_e;
-    }
+    if (++tap == NTAP) { tap = 0; ++c; }
   }
-  if constexpr (kStamp) {
-    const unsigned long long tot = stamp() - st_t0;
-    if (lane == 0 && a.dbg) {
-      unsigned long long* d = a.dbg + ((size_t)blockIdx.x * NW + wave) * 8;
-      d[0] = st_pro; d[1] = st_cmp; d[2] = st_wait; d[3] = st_epi; d[4] = tot; d[5] = st_steps; d[6] = 1;
-    }
-  }
+#pragma unroll
+  for (int h = 0; h < TC / 4; ++h)
+    conv_epilogue<T, T, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16, wp * TP,
+                              ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h, headw_s, headb_s);
 }
+
 
 // ---------------------------------------------------------------------------------
 // 3x3 conv, ring pipeline over 32-channel (64-byte) K chunks (the main kernel for 3x3 layers)
@@ -908,18 +519,6 @@ struct RingGeom {
 };
 
 // vmcnt(N) + barrier with N = nw * WI + (halo ? HI : 0), nw in [0, NS-2], as compile-time counts
-template <int N>
-__device__ __forceinline__ void wait_vm_only() {   // ablation: the wait without the barrier
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
-  asm volatile("" ::: "memory");
-}
-template <int WI, int HI, int NSM2>
-__device__ __forceinline__ void ring_wait_nobar(int nw, bool halo) {
-  if constexpr (NSM2 >= 2) { if (nw == 2) { if (halo) wait_vm_only<2 * WI + HI>(); else wait_vm_only<2 * WI>(); return; } }
-  if constexpr (NSM2 >= 1) { if (nw == 1) { if (halo) wait_vm_only<WI + HI>(); else wait_vm_only<WI>(); return; } }
-  if (halo) wait_vm_only<HI>(); else wait_vm_only<0>();
-}
 template <int WI, int HI, int NSM2>
 __device__ __forceinline__ void ring_wait(int nw, bool halo) {
   if constexpr (NSM2 >= 3) { if (nw == 3) { if (halo) wait_vm_barrier<3 * WI + HI>(); else wait_vm_barrier<3 * WI>(); return; } }
@@ -936,7 +535,9 @@ __device__ __forceinline__ void ring_wait(int nw, bool halo) {
 // MFMA (K = 9*C <= 27 padded to 32) and written to the halo buffer with ds_write, one chunk
 // ahead like the DMA halo; the window of the next tile is LDS-DMA'd (16-byte pieces, 2 pixels
 // per lane) into a single buffer after the current window's last use.
-template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0, int TPS = 1, int HS = 0>
+// TO / TQ: element types of the output / pooled map (default T), see conv_epilogue.
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS = 1, int HS = 0, typename TO = T,
+          typename TQ = TO>
 __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_ring_kernel(const IgemmArgs a) {
   using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS>;
   constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
@@ -1119,7 +720,7 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[4 * t + e] = (T)(inimg ? fmaxf(acc0[t][e] + b0v[cb][4 * t + e], 0.f) : 0.f);
+          for (int e = 0; e < 4; ++e) o[4 * t + e] = (T)(inimg ? relu_nan(acc0[t][e] + b0v[cb][4 * t + e]) : 0.f);
         if (real) *reinterpret_cast<uint4*>(dst + p * 64 + ((qq ^ (hx & 3)) << 4)) = __builtin_bit_cast(uint4, o);
       }
     }
@@ -1200,8 +801,7 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       int young = total - 2 - g;
       young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
       const bool hyoung = HS == 0 && wave < HLW && tap < NS - 2 && hseq + 1 < hseq_end;
-      if (ABL == 1 && tap != SPC - 1) ring_wait_nobar<TPS * WI, HI, NS - 2>(young, hyoung);   // ablation: barrier per chunk only
-      else ring_wait<TPS * WI, HI, NS - 2>(young, hyoung);
+      ring_wait<TPS * WI, HI, NS - 2>(young, hyoung);
     }
     bool tile_end = false;
     if (++tap == SPC) {
@@ -1217,7 +817,7 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       tile_of(item, n, ty, tx);
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<T, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
+        conv_epilogue<TO, TQ, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
                                   wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h,
                                   headw_s, headb_s);
 #pragma unroll
@@ -1241,12 +841,10 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
 // scatter epilogue.  LDS per slot: A [BR][64 B] (chunk q of row r at q ^ ((r >> 1) & 3)) +
 // B [256 px][64 B] (pixel row py*16+px, chunk q at q ^ ((py & 1) << 1): conflict-free for all
 // ds_read_b128 lane groups and pixel groups, checked exhaustively).
-// CTI = 1: a walker takes the n_ct row tiles of one pixel tile back to back (the B tile of row
-// tile ct > 0 is then re-read from L2 right after row tile 0 read it from HBM) instead of one
-// walker per row tile.  WRW = 2: 8 waves as 2 (rows) x 4 (pixels), a 256-row x 256-pixel block
-// tile (one block per CU): half the A + B LDS-DMA bytes per MFMA of the 128-row tile (the
-// large-Cin layers up4/up3 stream both operands from L2 at every step).
-template <typename T, int TCW, int NS, int CTI = 0, int WRW = 1>
+// WRW = 2: 8 waves as 2 (rows) x 4 (pixels), a 256-row x 256-pixel block tile (one block per
+// CU): half the A + B LDS-DMA bytes per MFMA of the 128-row tile (the large-Cin layers up4/up3
+// stream both operands from L2 at every step).  TO: element type of the scattered output.
+template <typename T, int TCW, int NS, int WRW = 1, typename TO = T>
 __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel(const IgemmArgs a) {
   constexpr int NW = 4 * WRW, TC = TCW, TP = 4, BR = 16 * TC * WRW, BKE = 64 / (int)sizeof(T);
   constexpr int WI = BR / (16 * NW);          // A DMA instructions per wave and step
@@ -1264,13 +862,12 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
     const int b = blockIdx.x, x = b & 7, k = b >> 3;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
   }
-  const int NCT = CTI ? a.n_ct : 1;                 // row tiles per pixel tile of one walker
-  const int ct0 = CTI ? 0 : bid % a.n_ct;
-  const int slot = CTI ? bid : bid / a.n_ct;
-  const int n_slots = CTI ? gridDim.x : gridDim.x / a.n_ct;
+  const int ct = bid % a.n_ct;                      // row tile of this walker
+  const int slot = bid / a.n_ct;
+  const int n_slots = gridDim.x / a.n_ct;
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
   if (slot >= n_mt) return;
-  const int items = NCT * ((n_mt - slot + n_slots - 1) / n_slots);
+  const int items = (n_mt - slot + n_slots - 1) / n_slots;
   const int H = a.H, W = a.W;
   const int S = a.Cin / BKE;
   const int total = items * S;
@@ -1279,9 +876,8 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
                      (wave * WI * 16 + (lane >> 2)) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
   const char* in = reinterpret_cast<const char*>(a.in);
   const char* zero = reinterpret_cast<const char*>(a.zero);
-  auto ct_of = [&](int i) { return CTI ? i - (i / NCT) * NCT : ct0; };
   auto tile_of = [&](int i, int& n, int& ty, int& tx) {
-    int mt = slot + (CTI ? i / NCT : i) * n_slots;
+    int mt = slot + i * n_slots;
     tx = mt % a.tiles_x;
     mt /= a.tiles_x;
     ty = mt % a.tiles_y;
@@ -1292,7 +888,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
     char* As = lds + (g % NS) * SLOT;
 #pragma unroll
     for (int j = 0; j < WI; ++j)
-      glds16(wblk + ((size_t)ct_of(i) * S + c) * ASLOT + j * 1024, As + (wave * WI + j) * 1024);
+      glds16(wblk + ((size_t)ct * S + c) * ASLOT + j * 1024, As + (wave * WI + j) * 1024);
     int n, ty, tx;
     tile_of(i, n, ty, tx);
 #pragma unroll
@@ -1361,10 +957,9 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
       c = 0;
       int n, ty, tx;
       tile_of(item, n, ty, tx);
-      const int ct = ct_of(item);
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<T, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
+        conv_epilogue<TO, TO, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
                                             tx * 16, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
                                             a.bias + ct * BR + wr * 16 * TC + 64 * h, nullptr,
                                             nullptr);
@@ -1375,20 +970,6 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
       ++item;
     }
   }
-}
-
-template <typename T, int TCW, int NS, int CTI = 0, int WRW = 1>
-static hipError_t launch_tring(const IgemmArgs& a, hipStream_t s) {
-  constexpr int BR = 16 * TCW * WRW, LDS = NS * (BR * 64 + 256 * 64);
-  if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
-  if (a.Cin % (64 / (int)sizeof(T)) || a.Ctot % BR || a.n_ct != a.Ctot / BR) return hipErrorInvalidValue;
-  const int n_mt = a.N * a.tiles_y * a.tiles_x;
-  const int nct = CTI ? 1 : a.n_ct;   // walkers per pixel-tile sequence
-  int n_slots = (kNumCUs * ((160 * 1024) / LDS)) / nct;
-  if (n_slots < 1) n_slots = 1;
-  if (n_slots > n_mt) n_slots = n_mt;
-  hipLaunchKernelGGL((convT_ring_kernel<T, TCW, NS, CTI, WRW>), dim3(nct * n_slots), dim3(256 * WRW), 0, s, a);
-  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------
@@ -1432,7 +1013,7 @@ __global__ __launch_bounds__(256) void first_conv_kernel(const FirstConvArgs a) 
       float s = 0.f;
 #pragma unroll
       for (int k = 0; k < KW; ++k) s = fmaf(ws[co * KW + k], xin[k], s);
-      v[e] = fmaxf(s + bs[co], 0.f);
+      v[e] = relu_nan(s + bs[co]);
     }
     store16<T>(dst + g * 16, v);
   }
@@ -1498,45 +1079,30 @@ __global__ __launch_bounds__(256) void first_conv_mfma_kernel(const FirstConvArg
       mfma_frag<T>(acc[t][p], af[t], bf);
     }
   }
-  conv_epilogue<T, 4, EPI_STORE>(e, acc, n, ty * 16, tx * 16, wave * 4, 0, bias_s, nullptr, nullptr);
+  conv_epilogue<T, T, 4, EPI_STORE>(e, acc, n, ty * 16, tx * 16, wave * 4, 0, bias_s, nullptr, nullptr);
 }
 
 // ---------------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------------
-template <typename T, int WR, int WPX, int TP, int TAPS, int EPI>
-static hipError_t launch_one(const IgemmArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((igemm_kernel<T, WR, WPX, TP, TAPS, EPI>), dim3(a.n_blocks), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-template <typename T, int WR, int WPX, int TCW, int HB, int NS, int PIPE, int EPI, int HSRC = 0, int KT = 3,
-          int TH = 16>
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int KT>
 static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
-  // HB=2: persistent grid, n_ct row tiles x n_slots pixel-tile walkers, as many blocks as
-  // fit per CU (LDS-limited).  HB=1: one block per (row tile, pixel tile).
-  using G = HaloGeom<T, WR, WPX, TCW, HB, NS, HSRC, KT, TH>;
-  if (a.tiles_y != (a.H + TH - 1) / TH) return hipErrorInvalidValue;   // host tiling must match
-  const int n_mt = a.N * a.tiles_y * a.tiles_x;
-  int n_slots = n_mt;
-  if (HB >= 2) {
-    n_slots = (kNumCUs * G::BLOCKS_PER_CU) / a.n_ct;
-    if (n_slots < 1) n_slots = 1;
-    if (n_slots > n_mt) n_slots = n_mt;
-  }
-  if (HSRC && (a.Cin != Elem<T>::BKE || a.c0 < 1 || a.c0 > 3 || !a.x0 || !a.w0p)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, HB, NS, PIPE, HSRC, KT, TH, EPI>), dim3(a.n_ct * n_slots),
-                     dim3(64 * WR * WPX), 0, s, a);
+  using G = HaloGeom<T, WR, WPX, TCW, NS, KT>;
+  if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
+  if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
+  const long long nb = (long long)a.n_ct * a.N * a.tiles_y * a.tiles_x;   // one block per (row tile, pixel tile)
+  if (nb <= 0 || nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, NS, KT, EPI>), dim3((unsigned)nb), dim3(64 * WR * WPX), 0,
+                     s, a);
   return hipGetLastError();
 }
 
-template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int ABL = 0, int TPS = 1, int HS = 0>
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ>
 static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
   using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS>;
   if constexpr (HS != 0) {
     if (a.Cin != 2 * G::BKE || a.c0 < 1 || a.c0 > 3 || !a.x0 || !a.w0p || !a.b0) return hipErrorInvalidValue;
   }
-  if constexpr (EPI == EPI_HEAD && G::BR != 64) return hipErrorInvalidValue;
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
   if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
@@ -1544,122 +1110,87 @@ static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
   int n_slots = (kNumCUs * per_cu) / a.n_ct;
   if (n_slots < 1) n_slots = 1;
   if (n_slots > n_mt) n_slots = n_mt;
-  if constexpr (EPI != EPI_HEAD || G::BR == 64)
-    hipLaunchKernelGGL((conv3x3_ring_kernel<T, WR, WPX, TCW, NS, EPI, ABL, TPS, HS>), dim3(a.n_ct * n_slots), dim3(64 * WR * WPX), 0,
-                       s, a);
+  hipLaunchKernelGGL((conv3x3_ring_kernel<T, WR, WPX, TCW, NS, EPI, TPS, HS, TO, TQ>), dim3(a.n_ct * n_slots),
+                     dim3(64 * WR * WPX), 0, s, a);
   return hipGetLastError();
 }
 
-template <typename T, int TAPS, int EPI>
-static hipError_t launch_cfg(int cfg, const IgemmArgs& a, hipStream_t s) {
-  if constexpr (TAPS == 9) {
-    switch (cfg) {
-      case CFG_HALO_R128_W4: return launch_halo<T, 2, 2, 4, 2, 3, 0, EPI>(a, s);
-      case CFG_HALO_R128_W8: return launch_halo<T, 2, 4, 4, 2, 3, 0, EPI>(a, s);
-      case CFG_HALO_R64_W4: return launch_halo<T, 1, 4, 4, 2, 3, 0, EPI>(a, s);
-      case CFG_HALO_R64_W8: return launch_halo<T, 1, 8, 4, 2, 3, 0, EPI>(a, s);
-      case CFG_HALO1_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 0, EPI>(a, s);
-      case CFG_HALO1_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 0, EPI>(a, s);
-      case CFG_HALO1_R128_W4: return launch_halo<T, 2, 2, 4, 1, 2, 0, EPI>(a, s);
-      case CFG_PHALO_R128_W8: return launch_halo<T, 2, 4, 4, 2, 3, 1, EPI>(a, s);
-      case CFG_PHALO1_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 1, EPI>(a, s);
-      case CFG_PHALO1_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 1, EPI>(a, s);
-      case CFG_HALO1_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 0, EPI>(a, s);
-      case CFG_HALO1_R128T8_NS3: return launch_halo<T, 1, 4, 8, 1, 3, 0, EPI>(a, s);
-      case CFG_T8_HALO1_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 0, EPI, 0, 3, 8>(a, s);
-      case CFG_T8_HALO_R64_W4: return launch_halo<T, 1, 4, 4, 2, 3, 0, EPI, 0, 3, 8>(a, s);
-      case CFG_T8_HALO_R64_W2: return launch_halo<T, 1, 2, 4, 2, 3, 0, EPI, 0, 3, 8>(a, s);
-      case CFG_HALO3_R64_W8: return launch_halo<T, 1, 8, 4, 3, 3, 0, EPI>(a, s);
-      case CFG_HALO3_R64_W4: return launch_halo<T, 1, 4, 4, 3, 3, 0, EPI>(a, s);
-      case CFG_SG_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 7, EPI>(a, s);
-      case CFG_SG_R128T8_NS3: return launch_halo<T, 1, 4, 8, 1, 3, 7, EPI>(a, s);
-      case CFG_SG_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 7, EPI>(a, s);
-      case CFG_SG_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 7, EPI>(a, s);
-      case CFG_RING_R128: return launch_ring<T, 1, 4, 8, 4, EPI>(a, s);
-      case CFG_RING_R64: return launch_ring<T, 1, 4, 4, 4, EPI>(a, s);
-      case CFG_RING_R128_NS3: return launch_ring<T, 1, 4, 8, 3, EPI>(a, s);
-      case CFG_RING_R64_NS5: return launch_ring<T, 1, 4, 4, 5, EPI>(a, s);
-      case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 0, 3>(a, s);
-      case CFG_RING_FUSED_IN:
-        if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 0, 3, 1>(a, s);
-        return hipErrorInvalidValue;
-      case CFG_FUSED_IN_W4:
-      case CFG_FUSED_IN_W8:
-        if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) {
-          if (cfg == CFG_FUSED_IN_W4) return launch_halo<T, 1, 4, 4, 1, 3, 0, EPI, 1>(a, s);
-          return launch_halo<T, 1, 8, 4, 1, 3, 0, EPI, 1>(a, s);
-        }
-        return hipErrorInvalidValue;
-#ifdef UNET_ABLATION   // timing-only builds: wrong outputs by construction
-      case CFG_COUNT + 0: return launch_halo<T, 1, 4, 4, 1, 3, 2, EPI>(a, s);   // HALO1_R64_W4, no MFMA
-      case CFG_COUNT + 1: return launch_halo<T, 1, 4, 4, 1, 3, 3, EPI>(a, s);   // HALO1_R64_W4, no DMA
-      case CFG_COUNT + 2: return launch_halo<T, 2, 4, 4, 2, 3, 2, EPI>(a, s);   // HALO_R128_W8, no MFMA
-      case CFG_COUNT + 3: return launch_halo<T, 2, 4, 4, 2, 3, 3, EPI>(a, s);   // HALO_R128_W8, no DMA
-      case CFG_COUNT + 4: return launch_halo<T, 1, 4, 4, 1, 3, 4, EPI>(a, s);   // HALO1_R64_W4, no DMA, no barrier
-      case CFG_COUNT + 5: return launch_halo<T, 1, 4, 4, 1, 3, 5, EPI>(a, s);   // PHALO1_R64_W4, no DMA
-      case CFG_COUNT + 6: return launch_halo<T, 1, 4, 4, 1, 3, 1, EPI>(a, s);   // PHALO1_R64_W4 (same binary A/B)
-      case CFG_COUNT + 7: return launch_halo<T, 1, 4, 4, 1, 3, 6, EPI>(a, s);   // stamped HALO1_R64_W4
-      case CFG_COUNT + 8: return launch_halo<T, 1, 8, 4, 1, 3, 6, EPI>(a, s);   // stamped HALO1_R64_W8
-      case CFG_COUNT + 9: return launch_halo<T, 1, 4, 8, 1, 2, 6, EPI>(a, s);   // stamped HALO1_R128T8_NS2
-      case CFG_COUNT + 10: return launch_halo<T, 1, 8, 4, 3, 3, 6, EPI>(a, s);  // stamped HALO3_R64_W8
-      case CFG_COUNT + 11: return launch_halo<T, 1, 4, 8, 1, 2, 8, EPI>(a, s);  // HALO1_R128T8_NS2, halo DMA only
-      case CFG_COUNT + 12: return launch_halo<T, 1, 4, 8, 1, 2, 9, EPI>(a, s);  // HALO1_R128T8_NS2, weight DMA only
-      case CFG_COUNT + 13: return launch_halo<T, 1, 4, 8, 1, 2, 3, EPI>(a, s);  // HALO1_R128T8_NS2, no DMA
-      case CFG_COUNT + 14: return launch_ring<T, 1, 4, 8, 4, EPI, 1>(a, s);      // RING_R128, barrier per chunk only
-#endif
-      default: break;
-    }
-  }
-  switch (cfg) {
-    case CFG_R128_P128: return launch_one<T, 2, 2, 4, TAPS, EPI>(a, s);
-    case CFG_R64_P128: return launch_one<T, 1, 4, 2, TAPS, EPI>(a, s);
-    case CFG_R64_P256: return launch_one<T, 1, 4, 4, TAPS, EPI>(a, s);
-    default: return hipErrorInvalidValue;
-  }
+template <typename T, int TCW, int NS, int WRW, typename TO>
+static hipError_t launch_tring(const IgemmArgs& a, hipStream_t s) {
+  constexpr int BR = 16 * TCW * WRW, LDS = NS * (BR * 64 + 256 * 64);
+  if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
+  if (a.Cin % (64 / (int)sizeof(T)) || a.Ctot % BR || a.n_ct != a.Ctot / BR) return hipErrorInvalidValue;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  int n_slots = (kNumCUs * ((160 * 1024) / LDS)) / a.n_ct;
+  if (n_slots < 1) n_slots = 1;
+  if (n_slots > n_mt) n_slots = n_mt;
+  hipLaunchKernelGGL((convT_ring_kernel<T, TCW, NS, WRW, TO>), dim3(a.n_ct * n_slots), dim3(256 * WRW), 0, s, a);
+  return hipGetLastError();
 }
 
-template <typename T>
-static hipError_t launch_t(int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s) {
-  if (taps == 9) {
-    switch (epi) {
-      case EPI_STORE: return launch_cfg<T, 9, EPI_STORE>(cfg, a, s);
-      case EPI_POOL: return launch_cfg<T, 9, EPI_POOL>(cfg, a, s);
-      case EPI_HEAD:
-        if (cfg_rows(cfg) != 64) return hipErrorInvalidValue;
-        return launch_cfg<T, 9, EPI_HEAD>(cfg, a, s);
-      default: return hipErrorInvalidValue;
-    }
-  }
-  if (taps == 1 && epi == EPI_UPSCATTER) {
-    switch (cfg) {   // ConvTranspose2d on the tile pipeline (no halo, 1 tap)
-      case CFG_HALO1_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
-      case CFG_HALO1_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 0, EPI_UPSCATTER, 0, 1>(a, s);
-      case CFG_HALO_R128_W8: return launch_halo<T, 2, 4, 4, 2, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
-      case CFG_HALO1_R64_W8: return launch_halo<T, 1, 8, 4, 1, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
-      case CFG_HALO1_R128T8_NS3: return launch_halo<T, 1, 4, 8, 1, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
-      case CFG_SG_R128T8_NS2: return launch_halo<T, 1, 4, 8, 1, 2, 7, EPI_UPSCATTER, 0, 1>(a, s);
-      case CFG_SG_R64_W4: return launch_halo<T, 1, 4, 4, 1, 3, 7, EPI_UPSCATTER, 0, 1>(a, s);
-      // persistent 3-deep ring: a 1-tap GEMM step is short, so the next chunk is fetched two
-      // steps ahead (the 2-deep ring must wait for its prefetch at the end of the same step)
-      case CFG_HALO_R128_W4: return launch_halo<T, 1, 4, 8, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
-      case CFG_HALO3_R64_W8: return launch_halo<T, 1, 8, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
-      case CFG_HALO3_R64_W4: return launch_halo<T, 1, 4, 4, 3, 3, 0, EPI_UPSCATTER, 0, 1>(a, s);
-      case CFG_TRING_R128: return launch_tring<T, 8, 3>(a, s);
-      case CFG_TRING_R128_CTI: return launch_tring<T, 8, 3, 1>(a, s);
-      case CFG_TRING_R256: return launch_tring<T, 8, 3, 0, 2>(a, s);
-      case CFG_TRING_R256_NS4: return launch_tring<T, 8, 4, 0, 2>(a, s);
-      default: return launch_cfg<T, 1, EPI_UPSCATTER>(cfg, a, s);
-    }
+// 3x3 layers.  T = operand type, TO / TQ = output / pooled-map types (the LDS-halo family runs
+// only with TO = TQ = T: it is the fp32 path).
+template <typename T, typename TO, typename TQ, int EPI>
+static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
+  constexpr bool same = std::is_same<T, TO>::value && std::is_same<TO, TQ>::value;
+  if (EPI == EPI_HEAD && cfg_rows(cfg) != 64) return hipErrorInvalidValue;   // the head needs all 64 channels
+  switch (cfg) {
+    case CFG_HALO_R64_W4: if constexpr (same) return launch_halo<T, 1, 4, 4, 3, EPI, 3>(a, s); break;
+    case CFG_HALO_R64_W8: if constexpr (same) return launch_halo<T, 1, 8, 4, 3, EPI, 3>(a, s); break;
+    case CFG_HALO_R128: if constexpr (same && EPI != EPI_HEAD) return launch_halo<T, 1, 4, 8, 2, EPI, 3>(a, s); break;
+    case CFG_RING_R128: if constexpr (EPI != EPI_HEAD) return launch_ring<T, 1, 4, 8, 3, EPI, 1, 0, TO, TQ>(a, s); break;
+    case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
+    case CFG_RING_FUSED_IN:
+      if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
+      break;
+    default: break;
   }
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_igemm(DType t, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s) {
-  switch (t) {
-    case DType::F32: return launch_t<float>(cfg, taps, epi, a, s);
-    case DType::BF16: return launch_t<__bf16>(cfg, taps, epi, a, s);
-    case DType::F16: return launch_t<_Float16>(cfg, taps, epi, a, s);
+// ConvTranspose2d(k2, s2) layers (1-tap GEMM + pixel-shuffle scatter).  TO = output type.
+template <typename T, typename TO>
+static hipError_t launch_up(int cfg, const IgemmArgs& a, hipStream_t s) {
+  switch (cfg) {
+    case CFG_HALO_R128:
+      if constexpr (std::is_same<T, TO>::value) return launch_halo<T, 1, 4, 8, 2, EPI_UPSCATTER, 1>(a, s);
+      break;
+    case CFG_TRING_R128: return launch_tring<T, 8, 3, 1, TO>(a, s);
+    case CFG_TRING_R256: return launch_tring<T, 8, 4, 2, TO>(a, s);
+    default: break;
   }
+  return hipErrorInvalidValue;
+}
+
+template <typename T, typename TO, typename TQ>
+static hipError_t launch_typed(int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s) {
+  if (taps == 9) {
+    switch (epi) {
+      case EPI_STORE: return launch_3x3<T, TO, TQ, EPI_STORE>(cfg, a, s);
+      case EPI_POOL: return launch_3x3<T, TO, TQ, EPI_POOL>(cfg, a, s);
+      case EPI_HEAD: return launch_3x3<T, TO, TQ, EPI_HEAD>(cfg, a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (taps == 1 && epi == EPI_UPSCATTER) return launch_up<T, TO>(cfg, a, s);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_igemm(DType t, DType to, DType tq, int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s) {
+  if (t == to && to == tq) {
+    switch (t) {
+      case DType::F32: return launch_typed<float, float, float>(cfg, taps, epi, a, s);
+      case DType::BF16: return launch_typed<__bf16, __bf16, __bf16>(cfg, taps, epi, a, s);
+      case DType::F16: return launch_typed<_Float16, _Float16, _Float16>(cfg, taps, epi, a, s);
+    }
+    return hipErrorInvalidValue;
+  }
+  // the mixed bf16 / fp16 plan's two seams (unet_capi.cpp): an fp16 pooled layer whose pooled map
+  // feeds a bf16 layer, and a bf16 ConvTranspose whose output feeds an fp16 layer
+  if (t == DType::F16 && to == DType::F16 && tq == DType::BF16 && taps == 9 && epi == EPI_POOL)
+    return launch_3x3<_Float16, _Float16, __bf16, EPI_POOL>(cfg, a, s);
+  if (t == DType::BF16 && to == DType::F16 && tq == DType::F16 && taps == 1 && epi == EPI_UPSCATTER)
+    return launch_up<__bf16, _Float16>(cfg, a, s);
   return hipErrorInvalidValue;
 }
 
@@ -1765,32 +1296,56 @@ hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, in
   return hipGetLastError();
 }
 
-// Network input pre-cast for the fused first conv of the ring kernel (HS = 1): fp32 NCHW
-// [N][C][H][W] -> element type T, 4 channels per pixel [N][H][W][4] (zero-padded), so a 20-pixel
-// window row is 160 contiguous bytes (10 LDS-DMA pieces).  The values are the (T) casts the
-// first conv's MFMA operand needs anyway.
+// Network input element (n, c, y, x) of the caller's tensor: fp32 or uint8 (value / 255, the
+// reference's np.float32 division, inference.py:40), NCHW or NHWC (include/unet_mi355x.h).
+__device__ __forceinline__ float input_at(const void* x, int layout, int xdt, long long n, int c, long long hw,
+                                          int C, long long HW) {
+  const long long i = layout == 0 ? (n * C + c) * HW + hw : (n * HW + hw) * C + c;
+  return xdt == 0 ? static_cast<const float*>(x)[i] : (float)static_cast<const uint8_t*>(x)[i] / 255.0f;
+}
+
+// Network input pre-cast for the fused first conv of the ring kernel (HS = 1): -> element type
+// T, 4 channels per pixel [N][H][W][4] (zero-padded), so a 20-pixel window row is 160 contiguous
+// bytes (10 LDS-DMA pieces).  The values are the (T) casts the first conv's MFMA operand needs.
 template <typename T>
-__global__ __launch_bounds__(256) void x_to_px4_kernel(const float* __restrict__ x, int N, int C, int H, int W,
-                                                      T* __restrict__ out) {
-  const long long P = (long long)N * H * W;
+__global__ __launch_bounds__(256) void x_to_px4_kernel(const void* __restrict__ x, int layout, int xdt, int N, int C,
+                                                      int H, int W, T* __restrict__ out) {
+  const long long HW = (long long)H * W, P = (long long)N * HW;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < P; i += (long long)gridDim.x * 256) {
-    const long long n = i / ((long long)H * W), hw = i - n * H * W;
+    const long long n = i / HW, hw = i - n * HW;
     typedef T t4 __attribute__((ext_vector_type(4)));
     t4 v;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = (T)(c < C ? x[(n * C + c) * H * W + hw] : 0.f);
+    for (int c = 0; c < 4; ++c) v[c] = (T)(c < C ? input_at(x, layout, xdt, n, c, hw, C, HW) : 0.f);
     reinterpret_cast<t4*>(out)[i] = v;
   }
 }
 
-hipError_t launch_x_to_px4(DType t, const float* x, int N, int C, int H, int W, void* out, hipStream_t s) {
+hipError_t launch_x_to_px4(DType t, const void* x, int layout, int xdt, int N, int C, int H, int W, void* out,
+                           hipStream_t s) {
   const dim3 grid(4096), block(256);
   if (t == DType::BF16)
-    hipLaunchKernelGGL(x_to_px4_kernel<__bf16>, grid, block, 0, s, x, N, C, H, W, static_cast<__bf16*>(out));
+    hipLaunchKernelGGL(x_to_px4_kernel<__bf16>, grid, block, 0, s, x, layout, xdt, N, C, H, W, static_cast<__bf16*>(out));
   else if (t == DType::F16)
-    hipLaunchKernelGGL(x_to_px4_kernel<_Float16>, grid, block, 0, s, x, N, C, H, W, static_cast<_Float16*>(out));
+    hipLaunchKernelGGL(x_to_px4_kernel<_Float16>, grid, block, 0, s, x, layout, xdt, N, C, H, W,
+                       static_cast<_Float16*>(out));
   else
     return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void x_to_nchw_f32_kernel(const void* __restrict__ x, int layout, int xdt, int N,
+                                                           int C, int H, int W, float* __restrict__ out) {
+  const long long HW = (long long)H * W, total = (long long)N * C * HW;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long hw = i % HW, nc = i / HW;
+    out[i] = input_at(x, layout, xdt, nc / C, (int)(nc % C), hw, C, HW);
+  }
+}
+
+hipError_t launch_x_to_nchw_f32(const void* x, int layout, int xdt, int N, int C, int H, int W, float* out,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(x_to_nchw_f32_kernel, dim3(4096), dim3(256), 0, s, x, layout, xdt, N, C, H, W, out);
   return hipGetLastError();
 }
 

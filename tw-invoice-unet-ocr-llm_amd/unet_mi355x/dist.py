@@ -9,6 +9,8 @@ code path.  The reference has no parallelism at all (single device, inference.py
 """
 from __future__ import annotations
 
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -20,10 +22,6 @@ def shard_bounds(n_total: int, rank: int, world: int) -> tuple[int, int]:
     base, extra = divmod(n_total, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
-
-
-def _backend(group=None) -> str:
-    return dist.get_backend(group) if dist.is_initialized() else "none"
 
 
 def all_gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
@@ -44,12 +42,7 @@ def all_gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tens
     else:
         send = local.contiguous()
     out = torch.empty((world * cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    if _backend(group) == "gloo":
-        parts = list(out.chunk(world, 0))
-        dist.all_gather(parts, send, group=group)
-        out = torch.cat(parts, 0)
-    else:
-        dist.all_gather_into_tensor(out, send, group=group)
+    dist.all_gather_into_tensor(out, send, group=group)   # RCCL over xGMI with "nccl"; gloo on CPU
     if n_total % world == 0:
         return out
     keep = []
@@ -81,3 +74,39 @@ class ShardedSegmenter:
             local = x_global_or_local[lo:hi]
         masks = self.segment_fn(local)
         return all_gather_rows(masks, n_total, self.group)
+
+
+def timed_steps(step, steps: int, warmup: int, sync=None, device=None, group=None) -> tuple[float, list]:
+    """The bench contract's timing loop (bench.py): ``warmup`` untimed steps, then exactly
+    ``steps`` timed steps bracketed by a barrier + ``sync()`` on both sides; returns the
+    elapsed seconds as the MAX over ranks (one all-reduce on ``device``: the GPU with "nccl",
+    the CPU with gloo) and the per-step host times of this rank.  ``step`` runs one step (for
+    N > 1 its forward and the mask all-gather)."""
+    sync = sync or (lambda: None)
+    distributed = dist.is_initialized() and dist.get_world_size(group) > 1
+    for _ in range(warmup):
+        step()
+    if distributed:
+        dist.barrier(group=group)
+    sync()
+    marks = [time.perf_counter()]
+    for _ in range(steps):
+        step()
+        marks.append(time.perf_counter())
+    sync()
+    if distributed:
+        dist.barrier(group=group)
+    elapsed = time.perf_counter() - marks[0]
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        elapsed = float(t.item())
+    return elapsed, [b - a for a, b in zip(marks, marks[1:])]
+
+
+def sharded_mask_step(segment_fn, x_local: torch.Tensor, masks_local: torch.Tensor, n_total: int, group=None):
+    """One data-parallel step of bench.py at N > 1: this rank's forward of its shard into its
+    (bit-packed) mask buffer, then the one exchange step -- the all-gather of every rank's masks.
+    Returns the gathered masks [n_total, ...] in global batch order."""
+    segment_fn(x_local, masks_local)
+    return all_gather_rows(masks_local, n_total, group)

@@ -49,8 +49,13 @@ class UNet(nn.Module):
     """unet_model.UNet(n_channels=3, n_classes=3) with an MI355X forward.
 
     compute_dtype: "fp32" (default; exact fp32 MFMA, reference semantics), "bf16" or
-    "fp16" (16-bit activations/weights, fp32 accumulation, fp32 head).  Default from
-    the UNET_MI355X_DTYPE environment variable.
+    "fp16" (16-bit activations/weights, fp32 accumulation, fp32 head), or "mixed" (bf16 at
+    resolution levels 2-4, fp16 at the full-resolution levels 0-1; the benchmark's plan, chosen
+    so the masks meet IoU >= 0.999 against fp32).  Default from the UNET_MI355X_DTYPE
+    environment variable.
+
+    Inference only: the native forward folds eval-mode BatchNorm and builds no autograd graph, so
+    calling it in training mode with grad enabled raises (use the reference module to train).
     """
 
     def __init__(self, n_channels: int = 3, n_classes: int = 3, compute_dtype: str | None = None,
@@ -117,6 +122,9 @@ class UNet(nn.Module):
 
     def _run(self, x: torch.Tensor, want_logits: bool, mask_kind: int, want_boxes: bool = False):
         self._check_input(x)
+        if self.training and torch.is_grad_enabled():
+            raise RuntimeError("unet_mi355x.UNet is inference-only (eval BatchNorm folded, no autograd); "
+                               "call .eval() or run under torch.no_grad()")
         h = self.native_handle(x.device)
         x = x.detach()
         if x.dtype != torch.float32 or not x.is_contiguous():
@@ -131,6 +139,7 @@ class UNet(nn.Module):
             masks = torch.empty((n, self.n_classes, hh, ww // 8), device=x.device, dtype=torch.uint8)
         stream = torch.cuda.current_stream(x.device).cuda_stream
         boxes = None
+        h.reserve(n, hh, ww)   # grows the workspace if needed (a no-op otherwise); forwards never allocate
         with torch.cuda.device(x.device):
             if want_boxes:
                 boxes = torch.empty((n, self.n_classes, 4), device=x.device, dtype=torch.int32)

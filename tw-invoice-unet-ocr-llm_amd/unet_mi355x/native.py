@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 import torch  # noqa: F401  (must precede the library load, see module docstring)
@@ -18,9 +19,11 @@ LIB_NAME = "libunet_mi355x.so"
 LIB_PATH = os.environ.get("UNET_MI355X_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 UNET_OK, UNET_EINVAL, UNET_ESHAPE, UNET_ENOMEM, UNET_EHIP, UNET_ESTATE, UNET_EKEY = 0, -1, -2, -3, -4, -5, -6
-DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16": 2}
+# "mixed": bf16 storage at resolution levels 2-4, fp16 at levels 0-1 (include/unet_mi355x.h)
+DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16": 2, "mixed": 3}
 MASK_NONE, MASK_U8, MASK_BITS = 0, 1, 2
-LAYOUT_NCHW, IN_F32 = 0, 0
+LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
+IN_F32, IN_U8 = 0, 1
 
 # every function include/unet_mi355x.h declares: name -> (restype, argtypes)
 _vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
@@ -48,6 +51,9 @@ SIGNATURES = {
     "unet_launch_label": (ctypes.c_char_p, [_vp, _i]),
     "unet_forward_timed": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
     "unet_debug_fetch": (_i, [_vp, ctypes.c_char_p, _vp, ctypes.POINTER(_sz), _vp]),
+    "unet_graph_create": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _i, ctypes.POINTER(_vp)]),
+    "unet_graph_launch": (_i, [_vp, _vp]),
+    "unet_graph_destroy": (_i, [_vp]),
     "unet_destroy": (_i, [_vp]),
     "unet_last_error": (ctypes.c_char_p, []),
     "unet_abi_version": (_i, []),
@@ -92,7 +98,9 @@ def check(rc: int, what: str):
 
 
 class Handle:
-    """One native handle = one device, one packed weight set, one workspace (not re-entrant)."""
+    """One native handle = one device, one packed weight set, one workspace.  Calls are serialised
+    on the host by ``lock``; on the device the library orders a call issued on another stream
+    after the previous one (include/unet_mi355x.h)."""
 
     def __init__(self, n_channels: int, n_classes: int, dtype: str, device: int,
                  thresholds=(0.25, 0.40, 0.30, 0.5)):
@@ -106,12 +114,19 @@ class Handle:
         check(self.lib.unet_create(ctypes.byref(cfg), ctypes.byref(h)), "unet_create")
         self._h = h
         self.lock = threading.Lock()
+        self._graphs = weakref.WeakSet()   # captured graphs die before the handle
 
     def load_weights(self, state_dict) -> None:
         """state_dict: mapping name -> torch.Tensor / np.ndarray (any device); strict."""
         keep, views = [], []
         for k, v in state_dict.items():
-            arr = v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v)
+            if isinstance(v, torch.Tensor):
+                v = v.detach().cpu()
+                # numpy has no bfloat16: a model cast with .to(torch.bfloat16) loads like the
+                # reference UNet does (its parameters are simply read back in fp32)
+                arr = (v.to(torch.float32) if v.is_floating_point() else v).numpy()
+            else:
+                arr = np.asarray(v)
             if arr.dtype.kind == "f":
                 arr = np.ascontiguousarray(arr, dtype=np.float32)
                 code = 0
@@ -132,23 +147,35 @@ class Handle:
         with self.lock:
             check(self.lib.unet_reserve(self._h, n, h, w), "unet_reserve")
 
+    @staticmethod
+    def _geometry(x: torch.Tensor, layout: int):
+        if x.dtype not in (torch.float32, torch.uint8) or not x.is_contiguous():
+            raise ValueError("x must be a contiguous float32 or uint8 tensor")
+        if layout == LAYOUT_NCHW:
+            n, c, h, w = x.shape
+        else:
+            n, h, w, c = x.shape
+        return n, h, w, IN_F32 if x.dtype == torch.float32 else IN_U8
+
     def forward(self, x: torch.Tensor, logits: torch.Tensor | None, masks: torch.Tensor | None,
-                mask_kind: int, stream: int) -> None:
-        n, c, h, w = x.shape
+                mask_kind: int, stream: int, layout: int = LAYOUT_NCHW) -> None:
+        """x: device [N, C, H, W] (layout NCHW) or [N, H, W, C] (NHWC), float32 or uint8 (/255).
+        The workspace must have been reserved for (N, H, W) (``reserve``)."""
+        n, h, w, xdt = self._geometry(x, layout)
         with self.lock:
-            check(self.lib.unet_forward(self._h, x.data_ptr(), LAYOUT_NCHW, IN_F32,
+            check(self.lib.unet_forward(self._h, x.data_ptr(), layout, xdt,
                                         None if logits is None else logits.data_ptr(),
                                         None if masks is None else masks.data_ptr(),
                                         mask_kind, n, h, w, stream), "unet_forward")
 
     def forward_boxes(self, x: torch.Tensor, logits: torch.Tensor | None, masks: torch.Tensor | None,
-                      mask_kind: int, boxes: torch.Tensor, stream: int) -> None:
+                      mask_kind: int, boxes: torch.Tensor, stream: int, layout: int = LAYOUT_NCHW) -> None:
         """forward + per-(image, field) mask boxes: int32 [N][n_classes][4] = x0, y0, x1, y1 (-1s if empty)."""
-        n, c, h, w = x.shape
+        n, h, w, xdt = self._geometry(x, layout)
         if boxes.dtype != torch.int32 or tuple(boxes.shape) != (n, self.n_classes, 4) or not boxes.is_contiguous():
             raise ValueError(f"boxes must be a contiguous int32 tensor of shape {(n, self.n_classes, 4)}")
         with self.lock:
-            check(self.lib.unet_forward_boxes(self._h, x.data_ptr(), LAYOUT_NCHW, IN_F32,
+            check(self.lib.unet_forward_boxes(self._h, x.data_ptr(), layout, xdt,
                                               None if logits is None else logits.data_ptr(),
                                               None if masks is None else masks.data_ptr(),
                                               mask_kind, boxes.data_ptr(), n, h, w, stream), "unet_forward_boxes")
@@ -165,17 +192,32 @@ class Handle:
                                            out.shape[1], out.shape[2], stream), "unet_preprocess")
 
     def forward_timed(self, x: torch.Tensor, logits: torch.Tensor | None, masks: torch.Tensor | None,
-                      mask_kind: int, stream: int) -> list:
+                      mask_kind: int, stream: int, layout: int = LAYOUT_NCHW) -> list:
         """forward + HIP-event time (ms) of every launch, in include/unet_mi355x.h order."""
-        n, c, h, w = x.shape
+        n, h, w, xdt = self._geometry(x, layout)
         nl = self.lib.unet_num_launches()
         ms = (ctypes.c_float * nl)()
         with self.lock:
-            check(self.lib.unet_forward_timed(self._h, x.data_ptr(), LAYOUT_NCHW, IN_F32,
+            check(self.lib.unet_forward_timed(self._h, x.data_ptr(), layout, xdt,
                                               None if logits is None else logits.data_ptr(),
                                               None if masks is None else masks.data_ptr(),
                                               mask_kind, n, h, w, stream, ms), "unet_forward_timed")
         return list(ms)
+
+    def graph(self, x: torch.Tensor, logits: torch.Tensor | None, masks: torch.Tensor | None, mask_kind: int,
+              boxes: torch.Tensor | None = None, layout: int = LAYOUT_NCHW) -> "Graph":
+        """Capture one forward over these fixed buffers into a hipGraph (unet_graph_create)."""
+        n, h, w, xdt = self._geometry(x, layout)
+        g = ctypes.c_void_p()
+        with self.lock:
+            check(self.lib.unet_graph_create(self._h, x.data_ptr(), layout, xdt,
+                                             None if logits is None else logits.data_ptr(),
+                                             None if masks is None else masks.data_ptr(), mask_kind,
+                                             None if boxes is None else boxes.data_ptr(), n, h, w,
+                                             ctypes.byref(g)), "unet_graph_create")
+        gr = Graph(self, g, (x, logits, masks, boxes))
+        self._graphs.add(gr)
+        return gr
 
     def launch_labels(self) -> list:
         """Kernel instantiation of every launch of a forward (include/unet_mi355x.h order)."""
@@ -192,9 +234,33 @@ class Handle:
               "unet_debug_fetch")
 
     def close(self) -> None:
+        for gr in list(getattr(self, "_graphs", ())):
+            gr.close()
         if getattr(self, "_h", None):
             self.lib.unet_destroy(self._h)
             self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Graph:
+    """A captured forward (unet_graph_*); keeps its buffers alive; replay with ``launch``."""
+
+    def __init__(self, handle: Handle, g: ctypes.c_void_p, buffers):
+        self.handle, self._g, self._buffers = handle, g, buffers
+
+    def launch(self, stream: int) -> None:
+        with self.handle.lock:
+            check(self.handle.lib.unet_graph_launch(self._g, stream), "unet_graph_launch")
+
+    def close(self) -> None:
+        if getattr(self, "_g", None):
+            self.handle.lib.unet_graph_destroy(self._g)
+            self._g = None
 
     def __del__(self):
         try:
