@@ -172,6 +172,22 @@ int unet_graph_create(unet_handle* h, const void* x, int x_layout, int x_dtype,
 int unet_graph_launch(unet_graph* g, void* hip_stream);
 int unet_graph_destroy(unet_graph* g);
 
+/* Multi-GPU data parallelism: one process per GPU, each rank runs
+ * unet_forward / unet_forward_boxes on its contiguous shard of the batch, and the one exchange
+ * step is an all-gather of the per-rank bit-packed masks (or boxes) over RCCL/xGMI.  These
+ * entry points give a C host that collective without torch.distributed; RCCL is loaded at run
+ * time (dlopen), so a host that never calls them never loads it.
+ *   rank 0: unet_comm_get_unique_id(id) -> send the UNET_COMM_ID_BYTES bytes to every rank
+ *   every rank: unet_comm_init(h, rank, nranks, id); ... unet_allgather(h, my_masks,
+ *     all_masks, bytes_per_rank, stream) (recv = nranks x bytes_per_rank, rank order);
+ *     unet_comm_destroy(h) (also done by unet_destroy).
+ * unet_allgather is stream-ordered like unet_forward (it follows the handle's previous call). */
+#define UNET_COMM_ID_BYTES 128
+int unet_comm_get_unique_id(void* id);
+int unet_comm_init(unet_handle* h, int rank, int nranks, const void* id);
+int unet_allgather(unet_handle* h, const void* send, void* recv, size_t bytes_per_rank, void* hip_stream);
+int unet_comm_destroy(unet_handle* h);
+
 int unet_destroy(unet_handle* h);
 
 /* Message of the last error on this thread ("" if none). */

@@ -73,3 +73,11 @@ def test_logit_cut_degenerate_thresholds():
     lib = native.load_library()
     assert lib.unet_logit_cut(1.0) == math.inf
     assert lib.unet_logit_cut(-0.5) == -math.inf
+
+
+def test_rccl_unique_id_without_gpu():
+    """The multi-GPU C-ABI extras load RCCL at run time (dlopen); the bootstrap id of rank 0 is
+    produced without a GPU (the all-gather itself is a -m gpu test)."""
+    from unet_mi355x import native
+    uid = native.Handle.comm_unique_id()
+    assert len(uid) == native.COMM_ID_BYTES and any(uid)

@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 TOL = {"fp32": 1e-4, "fp16": 5e-3, "bf16": 3.5e-2, "mixed": 3.5e-2}
 DEV = "cuda:0"
-HALO_CFGS, RING_CFGS, UP_CFGS = [0, 1, 2], [3, 4, 5], [2, 6, 7]   # csrc/unet_internal.h Cfg
+HALO_CFGS, RING_CFGS, UP_CFGS = [0, 1, 2], [3, 4, 5, 8, 9, 10], [2, 6, 7]   # csrc/unet_internal.h Cfg
 
 
 def make_model(sd_np, c, dtype):
@@ -310,6 +310,27 @@ def test_graph_replay_equals_eager():
     with pytest.raises(RuntimeError, match="stale"):
         g.launch(stream)
     g.close()
+    m.close()
+
+
+def test_rccl_allgather_c_abi_single_rank():
+    """unet_comm_init + unet_allgather (the C-ABI's RCCL all-gather of per-rank masks, SURVEY
+    §8b) on a one-rank communicator: the gathered buffer is the rank's masks, stream-ordered
+    after the forward that produced them."""
+    m = make_model(syn.make_state_dict(0, 3, 3, profile="pretrained"), 3, "mixed")
+    h = m.native_handle(torch.device(DEV))
+    x = torch.from_numpy(syn.invoice_pages(9, 2, 512, 512, 3)).to(DEV)
+    with torch.no_grad():
+        ref = m.forward_masks(x, packed=True).clone()
+    h.comm_init(0, 1, native.Handle.comm_unique_id())
+    masks = torch.empty_like(ref)
+    out = torch.zeros_like(ref)
+    stream = torch.cuda.current_stream().cuda_stream
+    h.forward(x, None, masks, native.MASK_BITS, stream)
+    h.allgather(masks, out, stream)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    h.comm_destroy()
     m.close()
 
 

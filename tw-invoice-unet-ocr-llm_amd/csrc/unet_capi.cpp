@@ -7,6 +7,8 @@
 #include "unet_internal.h"
 #include "../../include/unet_mi355x.h"
 
+#include <dlfcn.h>
+
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -96,8 +98,7 @@ struct unet_handle {
   DType dt = DType::BF16;   // storage element type of the workspace (bf16 / f16 plans: 2 bytes)
   float* w0 = nullptr;  // first conv folded fp32 [64][C][3][3]
   void* w0p = nullptr;  // first conv packed [64][32] (16-bit MFMA path, down1.3's operand type)
-  void* w0r = nullptr;  // the same, rows ordered for the ring kernel's fused first conv:
-                        // [cb][t][16][32], row (cb, t, r) = channel 32cb + 8(r>>2) + 4t + (r&3)
+  void* w0r = nullptr;  // the ring kernel's fused first conv: [cb][t][m][16 rows][16 k] (unet_load_weights)
   float* b0 = nullptr;
   Layer L[17];          // d1b d2a d2b d3a d3b d4a d4b bna bnb c4a c4b c3a c3b c2a c2b c1a c1b
   Layer U[4];           // up4 up3 up2 up1
@@ -120,6 +121,7 @@ struct unet_handle {
   hipStream_t last_stream = nullptr;
   bool pending = false;
   bool capturing = false;        // inside unet_graph_create: no event record / wait in the stream
+  void* comm = nullptr;          // RCCL communicator (unet_comm_init), ncclComm_t
   unsigned long long generation = 1;   // bumped whenever device pointers a graph captured change
 };
 
@@ -427,6 +429,10 @@ std::string layer_label(const Layer& L, int epi) {
   if (cfg_is_tring(cfg)) {
     std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, %d, %d, %s>", tname(L.dt), cfg == CFG_TRING_R256 ? 4 : 3,
                   cfg == CFG_TRING_R256 ? 2 : 1, tname(L.dto));
+  } else if (cfg_tile_w(cfg) == 32) {
+    std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, %d, %d, %d, %d, %d, %s, %s>", tname(L.dt), cfg_rows(cfg) / 16,
+                  ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING8_R64_WS ? 1 : 0, tname(L.dto),
+                  tname(epi == EPI_POOL ? L.dtq : L.dto));
   } else if (cfg_is_ring(cfg)) {
     std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %s, %s>", tname(L.dt),
                   cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0,
@@ -452,7 +458,7 @@ void build_labels(unet_handle* h) {
   for (int i = 0; i < UNET_NUM_LAUNCHES; ++i) {
     const int id = order[i];
     if (id < 0) {
-      h->labels[i] = h->L[D1B].cfg == CFG_RING_FUSED_IN ? std::string("x_to_px4_kernel<") + tname(t0) + ">" : buf;
+      h->labels[i] = h->L[D1B].cfg % 16 == CFG_RING_FUSED_IN ? std::string("x_to_px4_kernel<") + tname(t0) + ">" : buf;
       continue;
     }
     if (id >= 100) { h->labels[i] = layer_label(h->U[id - 100], EPI_UPSCATTER); continue; }
@@ -473,10 +479,47 @@ void parse_overrides(const char* ov, int n, int* cfg_out, bool (*ok)(int, int)) 
     const size_t colon = item.find(':');
     if (colon != std::string::npos) {
       const int li = std::atoi(item.substr(0, colon).c_str()), c = std::atoi(item.substr(colon + 1).c_str());
-      if (li >= 0 && li < n && c >= 0 && c < CFG_COUNT && ok(li, c)) cfg_out[li] = c;
+      if (li >= 0 && li < n && c >= 0 && c < cfg_limit() && ok(li, c)) cfg_out[li] = c;
     }
     pos = end + 1;
   }
+}
+
+// RCCL, resolved at run time (dlopen) so the library has no link-time dependency on it and a
+// host that never calls unet_comm_* never loads it.  ncclUniqueId is 128 opaque bytes.
+struct NcclId { char internal[UNET_COMM_ID_BYTES]; };
+struct Rccl {
+  void* lib = nullptr;
+  int (*get_unique_id)(NcclId*) = nullptr;
+  int (*comm_init_rank)(void**, int, NcclId, int) = nullptr;
+  int (*all_gather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
+  int (*comm_destroy)(void*) = nullptr;
+  const char* (*error_string)(int) = nullptr;
+};
+const Rccl* rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (tried) return r.lib ? &r : nullptr;
+  tried = true;
+  for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+    r.lib = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+    if (r.lib) break;
+  }
+  if (!r.lib) return nullptr;
+  r.get_unique_id = reinterpret_cast<int (*)(NcclId*)>(dlsym(r.lib, "ncclGetUniqueId"));
+  r.comm_init_rank = reinterpret_cast<int (*)(void**, int, NcclId, int)>(dlsym(r.lib, "ncclCommInitRank"));
+  r.all_gather = reinterpret_cast<int (*)(const void*, void*, size_t, int, void*, hipStream_t)>(dlsym(r.lib, "ncclAllGather"));
+  r.comm_destroy = reinterpret_cast<int (*)(void*)>(dlsym(r.lib, "ncclCommDestroy"));
+  r.error_string = reinterpret_cast<const char* (*)(int)>(dlsym(r.lib, "ncclGetErrorString"));
+  if (!r.get_unique_id || !r.comm_init_rank || !r.all_gather || !r.comm_destroy || !r.error_string) {
+    dlclose(r.lib);
+    r.lib = nullptr;
+    return nullptr;
+  }
+  return &r;
+}
+int rccl_fail(const Rccl* r, int rc, const char* what) {
+  return fail(UNET_EHIP, std::string(what) + ": " + (r ? r->error_string(rc) : "RCCL unavailable"));
 }
 
 }  // namespace
@@ -553,7 +596,9 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     // keep every layer on a configuration it supports, within the same kernel family (the
     // configurations of a family accumulate in the same K order, so they agree bitwise)
     const bool ring = cfg_is_ring(c);
-    if (c == CFG_RING_FUSED_IN && (i != D1B || f32)) c = L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128;
+    if (c % 16 == CFG_RING_FUSED_IN && (i != D1B || f32)) c = L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128;
+    if (c == CFG_RING8_R64_WS && (L.cin != 64 || f32)) c = L.cout == 64 ? CFG_RING8_R64_T3 : CFG_RING8_R128;   // 72 KB of weights max
+    if (c == CFG_RING8_R128 && L.cout == 64) c = CFG_RING8_R64_T3;
     if (cfg_rows(c) > L.cout || (i == C1B && cfg_rows(c) != 64))
       c = ring ? CFG_RING_R64_T3 : CFG_HALO_R64_W8;
     // the LDS-halo family stores its own operand type only: keep it off the mixed plan's seams
@@ -575,7 +620,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   DeviceGuard g(cfg->device);
   hipError_t e = hipEventCreateWithFlags(&h->done, hipEventDisableTiming);
   if (e != hipSuccess) { delete h; return fail(UNET_EHIP, std::string("hipEventCreate: ") + hipGetErrorString(e)); }
-  std::vector<uint8_t> z(256, 0);
+  std::vector<uint8_t> z(4096, 0);   // zero page: conv padding source, + 64 B per K chunk (ring halo cursors)
   int rc = upload(h, &h->zero, z.data(), z.size());
   if (rc) { free_all(h); (void)hipEventDestroy(h->done); delete h; return rc; }
   *out = h;
@@ -614,22 +659,37 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
     h->w0p = nullptr;
     h->w0r = nullptr;
     const DType t0 = h->L[D1B].dt;
-    if (t0 != DType::F32) {   // MFMA operand: [rho][k], k = c*9 + ky*3 + kx < 9C, zero pad to 32
-      std::vector<uint8_t> pk((size_t)64 * 32 * 2, 0);
+    if (t0 != DType::F32) {   // MFMA operand [t][m][16 rows][16 k] (first_conv_mfma_kernel), packed row
+      // rho = 16t + r = natural channel natural_of_packed(rho), k = 4q + c <-> tap 4m + q (< 9), channel c (< C)
+      std::vector<uint8_t> pk((size_t)4 * 3 * 16 * 16 * 2, 0);
       for (int rho = 0; rho < 64; ++rho) {
-        const int o = natural_of_packed(rho);
-        for (int k = 0; k < 9 * C; ++k) put_elem(t0, pk, (size_t)rho * 32 + k, w[(size_t)o * 9 * C + k]);
+        const int o = natural_of_packed(rho), tt = rho >> 4, r = rho & 15;
+        for (int m = 0; m < 3; ++m)
+          for (int q = 0; q < 4; ++q) {
+            const int tap = 4 * m + q;
+            if (tap >= 9) continue;
+            for (int c = 0; c < C; ++c)
+              put_elem(t0, pk, (((size_t)(tt * 3 + m) * 16 + r) * 16 + 4 * q + c), w[(size_t)o * 9 * C + c * 9 + tap]);
+          }
       }
       rc = upload(h, &h->w0p, pk.data(), pk.size());
       if (rc) return rc;
-      std::vector<uint8_t> pr((size_t)64 * 32 * 2, 0);
+      // the ring kernel's fused first conv: [cb][t][m][16 rows][16 k], row (cb, t, r) = channel
+      // 32cb + 8(r>>2) + 4t + (r&3), k = 4q + c <-> tap 4m + q (taps 9..11 zero), channel c (< C)
+      std::vector<uint8_t> pr((size_t)2 * 2 * 3 * 16 * 16 * 2, 0);
       for (int cb = 0; cb < 2; ++cb)
         for (int tt = 0; tt < 2; ++tt)
-          for (int r = 0; r < 16; ++r) {
-            const int o = 32 * cb + 8 * (r >> 2) + 4 * tt + (r & 3);
-            for (int k = 0; k < 9 * C; ++k)
-              put_elem(t0, pr, ((size_t)(cb * 2 + tt) * 16 + r) * 32 + k, w[(size_t)o * 9 * C + k]);
-          }
+          for (int m = 0; m < 3; ++m)
+            for (int r = 0; r < 16; ++r) {
+              const int o = 32 * cb + 8 * (r >> 2) + 4 * tt + (r & 3);
+              for (int q = 0; q < 4; ++q) {
+                const int tap = 4 * m + q;
+                if (tap >= 9) continue;
+                for (int c = 0; c < C; ++c)
+                  put_elem(t0, pr, ((((size_t)(cb * 2 + tt) * 3 + m) * 16 + r) * 16 + 4 * q + c),
+                           w[(size_t)o * 9 * C + c * 9 + tap]);
+              }
+            }
       rc = upload(h, &h->w0r, pr.data(), pr.size());
       if (rc) return rc;
     }
@@ -710,14 +770,14 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.ldo = ldo; a.out_off = out_off; a.ldo2 = ldo2;
   a.ncls = h->cfg.n_classes;
   a.mask_kind = mask_kind;
-  if (L.cfg == CFG_RING_FUSED_IN) {
+  if (L.cfg % 16 == CFG_RING_FUSED_IN) {
     a.x0 = x0;
     a.w0p = h->w0r;
     a.b0 = h->b0;
     a.c0 = h->cfg.n_channels;
   }
   for (int i = 0; i < kMaxClasses; ++i) a.thr_logit[i] = h->thr_logit[i];
-  a.tiles_x = (W + 15) / 16;
+  a.tiles_x = (W + cfg_tile_w(L.cfg) - 1) / cfg_tile_w(L.cfg);
   a.tiles_y = (H + 15) / 16;
   a.n_ct = L.ctot / cfg_rows(L.cfg);
   hipError_t e = launch_igemm(L.dt, L.dto, epi == EPI_POOL ? L.dtq : L.dto, L.cfg, L.taps, epi, a, s);
@@ -759,7 +819,7 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   // down1.net.0 (C -> 64): fused into down1.3 on the 16-bit ring path (fed by the pre-cast input),
   // a direct conv otherwise
   const void* x0 = x;
-  if (h->L[D1B].cfg == CFG_RING_FUSED_IN) {
+  if (h->L[D1B].cfg % 16 == CFG_RING_FUSED_IN) {
     hipError_t e = launch_x_to_px4(h->L[D1B].dt, x, x_layout, x_dtype, N, C, H, W, buf(B.xpx), s);
     if (e != hipSuccess) return fail(UNET_EHIP, std::string("input pre-cast launch: ") + hipGetErrorString(e));
     x0 = buf(B.xpx);
@@ -1021,10 +1081,59 @@ int unet_graph_destroy(unet_graph* gr) {
   return UNET_OK;
 }
 
+int unet_comm_get_unique_id(void* id) {
+  if (!id) return fail(UNET_EINVAL, "null argument");
+  const Rccl* r = rccl();
+  if (!r) return fail(UNET_EHIP, "RCCL (librccl.so) could not be loaded");
+  NcclId nid;
+  const int rc = r->get_unique_id(&nid);
+  if (rc) return rccl_fail(r, rc, "ncclGetUniqueId");
+  std::memcpy(id, &nid, sizeof nid);
+  return UNET_OK;
+}
+
+int unet_comm_init(unet_handle* h, int rank, int nranks, const void* id) {
+  if (!h || !id) return fail(UNET_EINVAL, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(UNET_EINVAL, "bad rank / nranks");
+  if (h->comm) return fail(UNET_ESTATE, "communicator already initialised");
+  const Rccl* r = rccl();
+  if (!r) return fail(UNET_EHIP, "RCCL (librccl.so) could not be loaded");
+  DeviceGuard g(h->cfg.device);
+  NcclId nid;
+  std::memcpy(&nid, id, sizeof nid);
+  const int rc = r->comm_init_rank(&h->comm, nranks, nid, rank);
+  if (rc) { h->comm = nullptr; return rccl_fail(r, rc, "ncclCommInitRank"); }
+  return UNET_OK;
+}
+
+int unet_allgather(unet_handle* h, const void* send, void* recv, size_t bytes_per_rank, void* stream) {
+  if (!h || !send || !recv) return fail(UNET_EINVAL, "null argument");
+  if (!h->comm) return fail(UNET_ESTATE, "no communicator: call unet_comm_init first");
+  const Rccl* r = rccl();
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  order_after_last(h, s);   // e.g. after this rank's forward on another stream
+  const int rc = r->all_gather(send, recv, bytes_per_rank, /*ncclUint8*/ 1, h->comm, s);
+  if (rc) return rccl_fail(r, rc, "ncclAllGather");
+  mark_done(h, s);
+  return UNET_OK;
+}
+
+int unet_comm_destroy(unet_handle* h) {
+  if (!h || !h->comm) return UNET_OK;
+  DeviceGuard g(h->cfg.device);
+  drain(h);
+  const Rccl* r = rccl();
+  const int rc = r ? r->comm_destroy(h->comm) : 0;
+  h->comm = nullptr;
+  return rc ? rccl_fail(r, rc, "ncclCommDestroy") : UNET_OK;
+}
+
 int unet_destroy(unet_handle* h) {
   if (!h) return UNET_OK;
   {
     DeviceGuard g(h->cfg.device);
+    if (h->comm) (void)unet_comm_destroy(h);
     free_all(h);
     if (h->done) (void)hipEventDestroy(h->done);
   }

@@ -31,7 +31,7 @@ struct IgemmArgs {
   const void* in;      // NHWC activations (element type T), pixel stride ldi
   const void* wgt;     // packed weights [Ctot][TAPS*Cin], rows permuted in 64-row groups
   const float* bias;   // [Ctot] natural row order (BN folded)
-  const void* zero;    // >= 256 zero bytes (source of the conv zero padding)
+  const void* zero;    // 4096 zero bytes (source of the conv zero padding; ring halos add 64 B per chunk)
   void* out;           // NHWC output, pixel stride ldo, channel offset out_off
   void* out2;          // EPI_POOL: pooled NHWC output (pixel stride ldo2)
   const float* head_w; // EPI_HEAD: [ncls][64] fp32
@@ -49,7 +49,7 @@ struct IgemmArgs {
   // fused first conv (halo computed from the raw input instead of loaded): down1.0 + down1.3
   const void* x0;      // network input: NCHW fp32 [N][c0][H][W] (halo kernel), or T [N][H][W][4]
                        // (CFG_RING_FUSED_IN, see launch_x_to_px4)
-  const void* w0p;     // first conv packed [64][32] element type (rows permuted)
+  const void* w0p;     // first conv packed [2][2][3][16][16] (unet_capi.cpp, CFG_RING_FUSED_IN)
   const float* b0;     // first conv folded bias [64]
   int c0;              // network input channels (1 or 3)
 };
@@ -57,8 +57,8 @@ struct IgemmArgs {
 struct FirstConvArgs {
   const float* x;      // NCHW fp32 input [N][C][H][W]
   const float* w;      // [64][C][3][3] folded (fp32 VALU path)
-  const void* wp;      // [64][32] packed element type, k = c*9 + ky*3 + kx, zero-padded,
-                       // rows permuted like the implicit-GEMM weights (MFMA path)
+  const void* wp;      // [4][3][16][16] packed element type: row tile t, MFMA m, packed row, k = 4q + c
+                       // (tap 4m + q, channel c; rows permuted like the implicit-GEMM weights)
   const float* b;      // [64] folded
   void* out;           // NHWC [N][H][W][64] element type T
   int N, C, H, W;
@@ -77,14 +77,20 @@ enum Cfg : int {
   CFG_RING_FUSED_IN = 5,  // RING_R64_T3 for down1.3 with down1.0 fused (halo chunks computed from the input)
   CFG_TRING_R128 = 6,     // ConvTranspose ring: 128-row x 256-pixel block tiles, 3 slots
   CFG_TRING_R256 = 7,     // ConvTranspose ring: 8 waves, 256-row x 256-pixel block tiles, 4 slots
-  CFG_COUNT = 8
+  // 8-wave ring over 16x32 pixel tiles, one block per CU (half the weight bytes per MFMA)
+  CFG_RING8_R128 = 8,     // 128 rows, one tap per step, 4 weight slots
+  CFG_RING8_R64_T3 = 9,   // 64 rows, 3 taps per step, 3 slots
+  CFG_RING8_R64_WS = 10,  // 64 rows, 3 taps per step, weight-stationary (Cin = 64)
+  CFG_COUNT = 11
 };
 int cfg_rows(int cfg);
 bool cfg_is_halo(int cfg);
 bool cfg_is_ring(int cfg);   // 64-byte-row ring kernel: step-major packed weights
 int ring_ns(int cfg);       // ring kernel: weight-ring slots
 int ring_tps(int cfg);      // ring kernel: taps per step
+int cfg_tile_w(int cfg);    // pixel-tile width (16, or 32 for the 8-wave ring)
 bool cfg_is_tring(int cfg); // ConvTranspose ring kernel: step-major packed weights
+int cfg_limit();            // valid Cfg values of this build (ablation builds: + 16 * ablation)
 
 // t: operand (activation + weight) type; to / tq: types of the output / pooled map (t unless
 // the layer sits at a seam of the mixed bf16/fp16 plan)

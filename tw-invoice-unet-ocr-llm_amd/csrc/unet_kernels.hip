@@ -31,17 +31,36 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef int frag_t __attribute__((ext_vector_type(4)));   // one 16-byte MFMA operand fragment
 
+// (ablation builds encode cfg = base + 16 * ablation; the helpers describe the base)
 int cfg_rows(int cfg) {
-  switch (cfg) {
-    case CFG_HALO_R128: case CFG_RING_R128: case CFG_TRING_R128: return 128;
+  switch (cfg % 16) {
+    case CFG_HALO_R128: case CFG_RING_R128: case CFG_TRING_R128: case CFG_RING8_R128: return 128;
     case CFG_TRING_R256: return 256;
     default: return 64;
   }
 }
 bool cfg_is_halo(int cfg) { return cfg == CFG_HALO_R64_W4 || cfg == CFG_HALO_R64_W8 || cfg == CFG_HALO_R128; }
-bool cfg_is_ring(int cfg) { return cfg == CFG_RING_R128 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN; }
-int ring_ns(int cfg) { (void)cfg; return 3; }
-int ring_tps(int cfg) { return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN) ? 3 : 1; }
+bool cfg_is_ring(int cfg) {
+  cfg %= 16;
+  return cfg == CFG_RING_R128 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R128 ||
+         cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS;
+}
+int cfg_tile_w(int cfg) {
+  cfg %= 16;
+  return (cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS) ? 32 : 16;
+}
+int ring_ns(int cfg) { return cfg % 16 == CFG_RING8_R128 ? 4 : 3; }
+int ring_tps(int cfg) {
+  cfg %= 16;
+  return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS) ? 3 : 1;
+}
+int cfg_limit() {
+#ifdef UNET_ABLATION
+  return CFG_COUNT + 16 * 5;
+#else
+  return CFG_COUNT;
+#endif
+}
 bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128 || cfg == CFG_TRING_R256; }
 
 // ---------------------------------------------------------------------------------
@@ -77,6 +96,22 @@ __device__ __forceinline__ void mfma_frag<float>(f32x4& acc, const uint4& a, con
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], acc, 0, 0, 0);
 }
+
+// 16x16x16 MFMA (K = 16: 4 values of 2 bytes per lane), the fused first conv's shape
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16(const uint2& a, const uint2& b, const f32x4& c);
+template <>
+__device__ __forceinline__ f32x4 mfma16<__bf16>(const uint2& a, const uint2& b, const f32x4& c) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4, a), __builtin_bit_cast(s4, b), c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma16<_Float16>(const uint2& a, const uint2& b, const f32x4& c) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4, a), __builtin_bit_cast(h4, b), c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma16<float>(const uint2&, const uint2&, const f32x4& c) { return c; }   // unused
 
 // torch semantics of ReLU / MaxPool2d: a NaN propagates (unet_model.py:12,16,34).  One
 // v_maximum3_f32 (IEEE-754-2019 maximum) each; fmaxf would turn a NaN into the other operand.
@@ -140,6 +175,13 @@ __device__ __forceinline__ void pix_of(int p, int& py, int& px) {
   py = 2 * (g >> 1) + (j >> 3);
   px = 8 * (g & 1) + (j & 7);
 }
+// the same for a 16 x TW tile (TW / 8 column groups per row pair)
+template <int TW>
+__device__ __forceinline__ void pix_of_w(int p, int& py, int& px) {
+  const int g = p >> 4, j = p & 15;
+  py = 2 * (g / (TW / 8)) + (j >> 3);
+  px = 8 * (g % (TW / 8)) + (j & 7);
+}
 
 // ---------------------------------------------------------------------------------
 // shared epilogue
@@ -165,7 +207,7 @@ __device__ __forceinline__ float xsum_lane32(float x) {   // x[l] + x[l ^ 32]
 
 // TO: element type of the NHWC output (and of the ConvTranspose scatter), TQ: of the pooled map
 // (the two differ where a layer feeds consumers of different storage type, see unet_capi.cpp).
-template <typename TO, typename TQ, int TP, int EPI>
+template <typename TO, typename TQ, int TP, int EPI, int TW = 16>
 __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0,
                                               int ox0, int g0, int row0, const float* bias_w,
                                               const float* head_w, const float* head_b) {
@@ -187,7 +229,7 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
 #pragma unroll
   for (int p = 0; p < TP; ++p) {
     int py, px;
-    pix_of((g0 + p) * 16 + col, py, px);
+    pix_of_w<TW>((g0 + p) * 16 + col, py, px);
     const int oy = oy0 + py, ox = ox0 + px;
     const bool inside = oy < H && ox < W;
     float v[16];
@@ -536,9 +578,11 @@ __device__ __forceinline__ void ring_wait(int nw, bool halo) {
 // ahead like the DMA halo; the window of the next tile is LDS-DMA'd (16-byte pieces, 2 pixels
 // per lane) into a single buffer after the current window's last use.
 // TO / TQ: element types of the output / pooled map (default T), see conv_epilogue.
-template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS = 1, int HS = 0, typename TO = T,
-          typename TQ = TO>
-__global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_ring_kernel(const IgemmArgs a) {
+// ABL (timing-only ablation builds, `make abl`; never in the product library): 1 = no barrier
+// in the loop, 2 = no MFMA, 3 = no fragment reads in the loop, 4 = no DMA in the loop, 5 = no
+// epilogue -- each gives wrong outputs by construction.
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ, int ABL>
+__device__ __forceinline__ void ring_body(const IgemmArgs& a) {
   using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS>;
   constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
   constexpr int HI = G::HI, WI = G::WI, HLW = G::HLW, HALO_BYTES = G::HALO_BYTES, WSLOT = G::WSLOT;
@@ -596,13 +640,15 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
     ty = mt % a.tiles_y;
     n = mt / a.tiles_y;
   };
-  auto issue_halo = [&](int hseq) {
-    if (wave >= HLW) return;   // (wave-uniform) not a halo loader
-    const int i = hseq / nch, c = hseq - (hseq / nch) * nch;
+  // Halo and weight DMAs are issued strictly in sequence (chunk after chunk, step after step), so
+  // both sources advance by cursors: the per-lane halo piece pointers are computed once per
+  // pixel tile (chunk c then adds 64c bytes; the zero page covers the invalid pieces of every
+  // chunk) and the weight source by one step -- no divisions or 64-bit address math per piece.
+  const char* hsrc[HI];
+  int hq_i = 0, hq_c = 0, hq_seq = 0;   // (tile, chunk, sequence number) of the next halo issue
+  auto halo_tile = [&](int i) {
     int n, ty, tx;
     tile_of(i, n, ty, tx);
-    char* dst = lds + (hseq & 1) * HALO_BYTES + wave * HI * 1024;
-    const long long c0 = (long long)c * BKE;
     const long long pix0 = (long long)(n * H + ty * 16) * W + tx * 16;
 #pragma unroll
     for (int j = 0; j < HI; ++j) {
@@ -612,18 +658,29 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       const bool ok = row < kRingPix && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       const int chk = ((lane & 3) ^ (hx & 3)) << 4;
       const long long pix = pix0 + (long long)(hy - 1) * W + (hx - 1);
-      const char* src = ok ? in + (pix * a.ldi + c0) * (long long)sizeof(T) + chk : zero + chk;
-      glds16(src, dst + j * 1024);
+      hsrc[j] = ok ? in + pix * a.ldi * (long long)sizeof(T) + chk : zero + chk;
     }
   };
-  auto issue_w = [&](int g) {
-    const int s = g - (g / S) * S;
-    const char* src = wblk + (size_t)s * SLOT;
-    char* dst = lds + WOFF + (g % NS) * SLOT + wave * WI * 1024;
+  auto issue_halo = [&]() {   // the next chunk in sequence
+    if (wave < HLW) {   // (wave-uniform) halo loader
+      if (hq_c == 0) halo_tile(hq_i);
+      char* dst = lds + (hq_seq & 1) * HALO_BYTES + wave * HI * 1024;
+#pragma unroll
+      for (int j = 0; j < HI; ++j) glds16(hsrc[j] + hq_c * 64, dst + j * 1024);
+    }
+    ++hq_seq;
+    if (++hq_c == nch) { hq_c = 0; ++hq_i; }
+  };
+  int wq_s = 0, wq_slot = 0;   // (step within the tile, ring slot) of the next weight issue
+  auto issue_w = [&]() {
+    const char* src = wblk + (size_t)wq_s * SLOT;
+    char* dst = lds + WOFF + wq_slot * SLOT + wave * WI * 1024;
 #pragma unroll
     for (int t = 0; t < TPS; ++t)
 #pragma unroll
       for (int j = 0; j < WI; ++j) glds16(src + t * WSLOT + j * 1024, dst + t * WSLOT + j * 1024);
+    if (++wq_s == S) wq_s = 0;
+    if (++wq_slot == NS) wq_slot = 0;
   };
 
   f32x4 acc[TC][TP];
@@ -662,37 +719,43 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       }
     }
   };
-  // halo chunk cb (channels 32cb .. 32cb+31 of down1.0's output) of tile i -> halo buffer hb
-  frag_t w0f[2][2];
+  // halo chunk cb (channels 32cb .. 32cb+31 of down1.0's output) of tile i -> halo buffer hb.
+  // The first conv runs as three 16x16x16 MFMAs per 16 pixels x 16 channels: K slot 4q + c of
+  // MFMA m is (tap 4m + q, channel c), so lane group q's B operand is ONE 8-byte ds_read_b64 of
+  // the 4-channel window pixel under its tap (taps 9..11 are zero): 3 reads per lane and pixel
+  // group instead of 8 scattered 2-byte gathers.  Weights: a.w0p = [cb][t][m][16 rows][16 k].
+  uint2 w0f[2][2][3];
   float b0v[2][8];
-  int xoff[8];
+  int toff[3];   // byte offset of this lane's tap in the window, per MFMA (-1: zero tap)
   if constexpr (HS != 0) {
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        w0f[cb][t] = *reinterpret_cast<const frag_t*>(reinterpret_cast<const char*>(a.w0p) +
-                                                      (((cb * 2 + t) * 16 + (lane & 15)) * 32 + 8 * (lane >> 4)) * sizeof(T));
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+          w0f[cb][t][m] = *reinterpret_cast<const uint2*>(
+              reinterpret_cast<const char*>(a.w0p) + ((((cb * 2 + t) * 3 + m) * 16 + (lane & 15)) * 16 + 4 * (lane >> 4)) * sizeof(T));
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int j = 0; j < 8; ++j) b0v[cb][j] = a.b0[32 * cb + 8 * (lane >> 4) + j];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {   // k = 8q + j -> (channel, ky, kx) offset in the window
-      const int k = 8 * (lane >> 4) + j, c = k / 9, r = k - (k / 9) * 9;
-      xoff[j] = k < 9 * a.c0 ? ((r / 3) * 20 + (r - (r / 3) * 3)) * 4 + c : -1;
+    for (int m = 0; m < 3; ++m) {
+      const int tp = 4 * m + (lane >> 4);
+      toff[m] = tp < 9 ? ((tp / 3) * 20 + (tp - (tp / 3) * 3)) * 4 * (int)sizeof(T) : -1;
     }
   }
   // part = 0 / 1: the even / odd pixel groups of this wave (the chunk is computed over two
   // steps, so that no single step carries all of it); at most 3 groups per part, unrolled so
-  // that the gathers of all of them are in flight together
+  // that the reads of all of them are in flight together
   constexpr int HGR = (kRingPix + 15) / 16;               // 16-pixel groups of the halo
   constexpr int HIT = (HGR + 2 * NW - 1) / (2 * NW);      // groups per wave and part
   auto compute_halo = [&](int i, int cb, int hb, int part) {
     if constexpr (HS != 0) {
       int n, ty, tx;
       tile_of(i, n, ty, tx);
-      const T* xs = reinterpret_cast<const T*>(lds + G::XS_OFF);
+      const char* xs = lds + G::XS_OFF;
       char* dst = lds + hb * HALO_BYTES;
       const int qq = lane >> 4;
 #pragma unroll
@@ -702,20 +765,19 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
         const int p = grp * 16 + (lane & 15);
         const bool real = p < kRingPix;
         const int hy = real ? p / 18 : 0, hx = real ? p - (p / 18) * 18 : 0;
-        typedef T t8 __attribute__((ext_vector_type(8)));
-        t8 hv;
+        const char* px = xs + (hy * 20 + hx) * 4 * (int)sizeof(T);
+        f32x4 acc0[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hv[j] = xoff[j] >= 0 ? xs[(hy * 20 + hx) * 4 + xoff[j]] : (T)0.f;
-        const uint4 bfr = __builtin_bit_cast(uint4, hv);
-        f32x4 acc0[2];
+        for (int m = 0; m < 3; ++m) {
+          uint2 bv = *reinterpret_cast<const uint2*>(px + (toff[m] < 0 ? 0 : toff[m]));
+          if (toff[m] < 0) bv = uint2{0u, 0u};   // 0 x (a NaN input) must stay 0
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-          mfma_frag<T>(acc0[t], __builtin_bit_cast(uint4, w0f[cb][t]), bfr);
+          for (int t = 0; t < 2; ++t) acc0[t] = mfma16<T>(w0f[cb][t][m], bv, acc0[t]);
         }
         // lane holds channels 32cb + 8q + 4t + e: 8 consecutive channels = one 16-byte piece
         const int iy = ty * 16 + hy - 1, ix = tx * 16 + hx - 1;
         const bool inimg = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        typedef T t8 __attribute__((ext_vector_type(8)));
         t8 o;
 #pragma unroll
         for (int t = 0; t < 2; ++t)
@@ -733,11 +795,11 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
     compute_halo(0, 0, 0, 0);
     compute_halo(0, 0, 0, 1);
   } else {
-    issue_halo(0);
+    issue_halo();
   }
 #pragma unroll
   for (int k = 0; k < NS - 1; ++k)
-    if (k < total) issue_w(k);
+    if (k < total) issue_w();
   for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];
   if (EPI == EPI_HEAD) {
     for (int i = tid; i < a.ncls * 64; i += 64 * NW) headw_s[i] = a.head_w[i];
@@ -750,11 +812,29 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
 
   // one step: A (weight) fragments stream through a 3-register ring two MFMA groups ahead;
   // sched_group_barrier pins the read/MFMA interleave (see step_sg above)
+  frag_t abl_fr[2];   // ablation 3: the fragments every MFMA reads
+  if constexpr (ABL == 3) {
+    abl_fr[0] = *reinterpret_cast<const frag_t*>(lds + WOFF + lane * 16);
+    abl_fr[1] = *reinterpret_cast<const frag_t*>(lds + lane * 16);
+  }
   auto step = [&](int g, int hs, int tp, int tsub) {
     const int dy = tp / 3, dx = tp - (tp / 3) * 3;
     const char* Hs = lds + (hs & 1) * HALO_BYTES + (dy * 18 + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
     const char* Ws = wrow + (g % NS) * SLOT + tsub * WSLOT;
     frag_t bq[TP], ar[3];
+    if constexpr (ABL == 3) {   // ablation: fragments from registers only
+#pragma unroll
+      for (int p = 0; p < TP; ++p) { bq[p] = abl_fr[p & 1]; asm volatile("" : "+v"(bq[p])); }
+#pragma unroll
+      for (int t = 0; t < TC; ++t) {
+        frag_t af = abl_fr[t & 1];
+        asm volatile("" : "+v"(af));
+#pragma unroll
+        for (int p = 0; p < TP; ++p)
+          mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
+      }
+      return;
+    }
 #pragma unroll
     for (int p = 0; p < TP; ++p) bq[p] = *reinterpret_cast<const frag_t*>(Hs + prow[p]);
     ar[0] = *reinterpret_cast<const frag_t*>(Ws);
@@ -765,8 +845,10 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       if (t + 2 < TC) ar[(t + 2) % 3] = *reinterpret_cast<const frag_t*>(Ws + (t + 2) * 16 * 64);
       const frag_t af = ar[t % 3];
 #pragma unroll
-      for (int p = 0; p < TP; ++p)
-        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
+      for (int p = 0; p < TP; ++p) {
+        if constexpr (ABL == 2) asm volatile("" ::"v"(af), "v"(bq[p]));   // ablation: no MFMA
+        else mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
+      }
       if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
     }
@@ -775,11 +857,11 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
   int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
   for (int g = 0; g < total; ++g) {
     const bool hnext = tap == 0 && hseq + 1 < hseq_end;
-    if constexpr (HS == 0) {
-      if (hnext) issue_halo(hseq + 1);
+    if constexpr (HS == 0 && ABL != 4) {
+      if (hnext) issue_halo();
     }
-    if (g + NS - 1 < total) issue_w(g + NS - 1);
-    if constexpr (HS != 0) {
+    if (ABL != 4 && g + NS - 1 < total) issue_w();
+    if constexpr (HS != 0 && ABL != 4) {
       // the next tile's window, once this tile's last halo chunk has been computed from it (at
       // chunk 0, steps 0 and 1; the barrier after step 1 retired every read of xs).  Issued
       // after this step's weights, so the wait at the end of the NEXT step (for those weights)
@@ -801,7 +883,288 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       int young = total - 2 - g;
       young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
       const bool hyoung = HS == 0 && wave < HLW && tap < NS - 2 && hseq + 1 < hseq_end;
-      ring_wait<TPS * WI, HI, NS - 2>(young, hyoung);
+      if constexpr (ABL == 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // ablation: no barrier
+      else if constexpr (ABL == 4) wait_vm_barrier<0>();
+      else ring_wait<TPS * WI, HI, NS - 2>(young, hyoung);
+    }
+    bool tile_end = false;
+    if (++tap == SPC) {
+      tap = 0;
+      ++hseq;
+      if (++c == nch) {
+        c = 0;
+        tile_end = true;
+      }
+    }
+    if (tile_end) {
+      int n, ty, tx;
+      tile_of(item, n, ty, tx);
+      if constexpr (ABL == 5) {   // ablation: no epilogue (keep the accumulators alive)
+#pragma unroll
+        for (int t = 0; t < TC; ++t)
+#pragma unroll
+          for (int p = 0; p < TP; ++p) asm volatile("" ::"v"(acc[t][p]));
+      } else {
+#pragma unroll
+      for (int h = 0; h < TC / 4; ++h)
+        conv_epilogue<TO, TQ, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
+                                  wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h,
+                                  headw_s, headb_s);
+      }
+#pragma unroll
+      for (int t = 0; t < TC; ++t)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ++item;
+    }
+  }
+}
+
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS = 1, int HS = 0, typename TO = T,
+          typename TQ = TO>
+__global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_ring_kernel(const IgemmArgs a) {
+  ring_body<T, WR, WPX, TCW, NS, EPI, TPS, HS, TO, TQ, 0>(a);
+}
+#ifdef UNET_ABLATION
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ, int ABL>
+__global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_ring_abl_kernel(const IgemmArgs a) {
+  ring_body<T, WR, WPX, TCW, NS, EPI, TPS, HS, TO, TQ, ABL>(a);
+}
+#endif
+
+// ---------------------------------------------------------------------------------
+// 3x3 conv, 8-wave ring over 16 x 32 pixel tiles (one block per CU)
+// ---------------------------------------------------------------------------------
+// Ablations of the 4-wave ring (profiles/tune_r2_ablation.txt) show the L2 -> LDS stream as the
+// limiter of the layers with few output channels: without the in-loop LDS-DMA conv1.0 runs 40 %
+// faster, conv1.3 33 %, the 128-row layers 14-29 %, while dropping the LDS fragment reads or the
+// barriers changes almost nothing.  Per MFMA a 64-row x 256-pixel block tile streams ~100 B of
+// weights + halo into LDS (the weights dominate: they are re-fetched for every pixel tile).
+// This variant doubles the pixel tile (16 x 32, 512 pixels, 8 waves = 2 per SIMD of ONE block per
+// CU, 64 pixels per wave as before), so every weight byte feeds twice the MFMAs and the halo
+// overlap shrinks (18x34 / 512 = 1.20 vs 1.27).  WST = 1 (weight-stationary, Cin = 64 layers):
+// all of the row tile's weights (6 steps x 12 KB = 72 KB) are DMA'd once per block and stay in
+// LDS; the loop then streams only the halo, and needs a barrier only at chunk ends.
+// LDS: [halo 0][halo 1][weights: NS slots, or all S steps (WST)][bias/head params].
+// Same K order (chunk32-major, tap-minor), fragment layouts and swizzles as the 4-wave ring (the
+// 34-pixel halo row stride is 544 dwords = 32 mod 64 banks, like the 18-pixel one), so the two
+// agree bitwise.
+template <typename T, int TCW, int NS, int TPS, int WST>
+struct Ring8Geom {
+  static constexpr int NW = 8, TW = 32, TP = 4;
+  static constexpr int TC = TCW;
+  static constexpr int BR = 16 * TC;
+  static constexpr int BKE = 64 / (int)sizeof(T);
+  static constexpr int HWD = TW + 2;                  // halo width (34)
+  static constexpr int HP = 18 * HWD;                 // halo pixels (612)
+  static constexpr int HI = (HP + 16 * NW - 1) / (16 * NW);   // halo DMA instructions per wave (5)
+  static constexpr int HALO_BYTES = HI * NW * 16 * 64;
+  static constexpr int WSLOT = BR * 64;               // one tap's weights
+  static constexpr int SLOT = TPS * WSLOT;            // one step
+  static constexpr int PIECES = SLOT / 1024;          // weight DMA instructions per step (all waves)
+  static constexpr int WST_STEPS = 6;                 // weight-stationary capacity: Cin = 64, 3 taps/step
+  static constexpr int WBYTES = WST ? WST_STEPS * SLOT : NS * SLOT;
+  static constexpr int WOFF = 2 * HALO_BYTES;
+  static constexpr int PARAM_OFF = WOFF + WBYTES;
+  static constexpr int LDS_BYTES = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier_rt_case() { wait_vm_barrier<N>(); }
+// vmcnt(n) + barrier for a runtime (wave-uniform) n in [0, 15]
+__device__ __forceinline__ void wait_vm_barrier_rt(int n) {
+  switch (n) {
+    case 0: wait_vm_barrier<0>(); break;   case 1: wait_vm_barrier<1>(); break;
+    case 2: wait_vm_barrier<2>(); break;   case 3: wait_vm_barrier<3>(); break;
+    case 4: wait_vm_barrier<4>(); break;   case 5: wait_vm_barrier<5>(); break;
+    case 6: wait_vm_barrier<6>(); break;   case 7: wait_vm_barrier<7>(); break;
+    case 8: wait_vm_barrier<8>(); break;   case 9: wait_vm_barrier<9>(); break;
+    case 10: wait_vm_barrier<10>(); break; case 11: wait_vm_barrier<11>(); break;
+    case 12: wait_vm_barrier<12>(); break; case 13: wait_vm_barrier<13>(); break;
+    case 14: wait_vm_barrier<14>(); break; default: wait_vm_barrier<15>(); break;
+  }
+}
+
+template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ>
+__global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a) {
+  using G = Ring8Geom<T, TCW, NS, TPS, WST>;
+  constexpr int NW = G::NW, TW = G::TW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
+  constexpr int HWD = G::HWD, HP = G::HP, HI = G::HI, HALO_BYTES = G::HALO_BYTES;
+  constexpr int WSLOT = G::WSLOT, SLOT = G::SLOT, PIECES = G::PIECES, WOFF = G::WOFF;
+  constexpr int SPC = 9 / TPS;   // steps per 32-channel chunk
+  static_assert(TPS == 1 || TPS == 3, "taps per step");
+  static_assert(WST || (NS >= 3 && NS <= 4), "weight ring depth");
+  static_assert(EPI != EPI_HEAD || BR == 64, "fused head needs the 64 channels in one block");
+  static_assert(G::LDS_BYTES <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
+  float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
+  float* headw_s = bias_s + BR;
+  float* headb_s = headw_s + kMaxClasses * 64;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wp = wave;   // all 8 waves split the pixels; each covers all BR rows
+
+  int bid;
+  {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one pixel-tile walker
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
+    const int b = blockIdx.x, x = b & 7, k = b >> 3;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  }
+  const int ct = bid % a.n_ct;
+  const int slot = bid / a.n_ct;
+  const int n_slots = gridDim.x / a.n_ct;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  if (slot >= n_mt) return;
+  const int items = (n_mt - slot + n_slots - 1) / n_slots;
+
+  const int H = a.H, W = a.W;
+  const int nch = a.Cin / BKE;
+  const int S = SPC * nch;
+  const int total = items * S;
+  const int hseq_end = items * nch;
+  // weight DMA pieces of this wave per step: pieces wave, wave + 8, ... of the step's PIECES
+  const int wcnt = (PIECES - wave + NW - 1) / NW;
+
+  // weights of row tile ct in step order (the 4-wave ring's packing): piece j of a step = rows
+  // 16j .. 16j+15; per lane one 16-byte chunk of row 16j + lane/4 at position chunk ^ ((row>>1)&3)
+  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * SLOT + (lane >> 2) * 64 +
+                     (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
+  const char* in = reinterpret_cast<const char*>(a.in);
+  const char* zero = reinterpret_cast<const char*>(a.zero);
+
+  auto tile_of = [&](int i, int& n, int& ty, int& tx) {
+    int mt = slot + i * n_slots;
+    tx = mt % a.tiles_x;
+    mt /= a.tiles_x;
+    ty = mt % a.tiles_y;
+    n = mt / a.tiles_y;
+  };
+  // sequential cursors, as in the 4-wave ring (per-lane halo pointers computed once per tile)
+  const char* hsrc[HI];
+  int hq_i = 0, hq_c = 0, hq_seq = 0;
+  auto issue_halo = [&]() {
+    if (hq_c == 0) {
+      int n, ty, tx;
+      tile_of(hq_i, n, ty, tx);
+      const long long pix0 = (long long)(n * H + ty * 16) * W + tx * TW;
+#pragma unroll
+      for (int j = 0; j < HI; ++j) {
+        const int row = (wave * HI + j) * 16 + (lane >> 2);
+        const int hy = row / HWD, hx = row - (row / HWD) * HWD;
+        const int iy = ty * 16 + hy - 1, ix = tx * TW + hx - 1;
+        const bool ok = row < HP && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        const int chk = ((lane & 3) ^ (hx & 3)) << 4;
+        const long long pix = pix0 + (long long)(hy - 1) * W + (hx - 1);
+        hsrc[j] = ok ? in + pix * a.ldi * (long long)sizeof(T) + chk : zero + chk;
+      }
+    }
+    char* dst = lds + (hq_seq & 1) * HALO_BYTES + wave * HI * 1024;
+#pragma unroll
+    for (int j = 0; j < HI; ++j) glds16(hsrc[j] + hq_c * 64, dst + j * 1024);
+    ++hq_seq;
+    if (++hq_c == nch) { hq_c = 0; ++hq_i; }
+  };
+  // weights of step s into LDS slot `dst_slot` (this wave's pieces)
+  auto issue_w_step = [&](int s, int dst_slot) {
+    const char* src = wblk + (size_t)s * SLOT;
+    char* dst = lds + WOFF + dst_slot * SLOT;
+#pragma unroll
+    for (int k = 0; k < (PIECES + NW - 1) / NW; ++k) {
+      const int j = wave + k * NW;
+      if (j < PIECES) glds16(src + j * 1024, dst + j * 1024);   // wave-uniform
+    }
+  };
+  int wq_s = 0, wq_slot = 0;
+  auto issue_w = [&]() {
+    issue_w_step(wq_s, wq_slot);
+    if (++wq_s == S) wq_s = 0;
+    if (++wq_slot == NS) wq_slot = 0;
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int t = 0; t < TC; ++t)
+#pragma unroll
+    for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int col = lane & 15, q = lane >> 4;
+  int prow[TP];
+#pragma unroll
+  for (int p = 0; p < TP; ++p) {
+    int py, px;
+    pix_of_w<TW>((wp * TP + p) * 16 + col, py, px);
+    prow[p] = (py * HWD + px) * 64;
+  }
+  const int px_lane = col & 7;
+  const int wpos = (q ^ ((col >> 1) & 3)) << 4;
+  const char* wrow = lds + WOFF + col * 64 + wpos;
+
+  // prologue: halo of chunk 0; weights (all steps, or steps 0 .. NS-2); epilogue parameters
+  issue_halo();
+  if constexpr (WST) {
+    for (int s = 0; s < S; ++s) issue_w_step(s, s);
+  } else {
+#pragma unroll
+    for (int k = 0; k < NS - 1; ++k)
+      if (k < total) issue_w();
+  }
+  for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];
+  if (EPI == EPI_HEAD) {
+    for (int i = tid; i < a.ncls * 64; i += 64 * NW) headw_s[i] = a.head_w[i];
+    if (tid < a.ncls) headb_s[tid] = a.head_b[tid];
+  }
+  if constexpr (WST) {
+    wait_vm_barrier<0>();
+  } else {
+    const int young = total - 1 < NS - 2 ? total - 1 : NS - 2;   // W(1..NS-2) may stay in flight
+    wait_vm_barrier_rt(young * wcnt);
+  }
+
+  auto step = [&](int g, int hs, int tp, int tsub) {
+    const int dy = tp / 3, dx = tp - (tp / 3) * 3;
+    const char* Hs = lds + (hs & 1) * HALO_BYTES + (dy * HWD + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
+    const int ws = WST ? g - (g / S) * S : g % NS;
+    const char* Ws = wrow + ws * SLOT + tsub * WSLOT;
+    frag_t bq[TP], ar[3];
+#pragma unroll
+    for (int p = 0; p < TP; ++p) bq[p] = *reinterpret_cast<const frag_t*>(Hs + prow[p]);
+    ar[0] = *reinterpret_cast<const frag_t*>(Ws);
+    if (TC > 1) ar[1] = *reinterpret_cast<const frag_t*>(Ws + 16 * 64);
+    __builtin_amdgcn_sched_group_barrier(0x100, TP + (TC > 1 ? 2 : 1), 0);
+#pragma unroll
+    for (int t = 0; t < TC; ++t) {
+      if (t + 2 < TC) ar[(t + 2) % 3] = *reinterpret_cast<const frag_t*>(Ws + (t + 2) * 16 * 64);
+      const frag_t af = ar[t % 3];
+#pragma unroll
+      for (int p = 0; p < TP; ++p)
+        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
+      if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+    }
+  };
+
+  int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
+  for (int g = 0; g < total; ++g) {
+    const bool hnext = tap == 0 && hseq + 1 < hseq_end;
+    if (hnext) issue_halo();
+    if (!WST && g + NS - 1 < total) issue_w();
+#pragma unroll
+    for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
+    const bool chunk_end = tap == SPC - 1;
+    if constexpr (WST) {
+      // only the halo streams: the next chunk's halo (issued at this chunk's first step) must
+      // have landed, and every wave must be done with this chunk's halo before the next issue
+      if (chunk_end) wait_vm_barrier<0>();
+    } else {
+      // W(g+1) must have landed (and, at a chunk end, the next halo -- issued SPC-1 steps
+      // earlier, older than W(g+1)).  Younger loads may stay in flight: W(g+2 .. g+NS-1) and a
+      // halo issued within the last NS-2 steps.
+      int young = total - 2 - g;
+      young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
+      const bool hyoung = tap < NS - 2 && hseq + 1 < hseq_end;
+      wait_vm_barrier_rt(young * wcnt + (hyoung ? HI : 0));
     }
     bool tile_end = false;
     if (++tap == SPC) {
@@ -817,9 +1180,8 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       tile_of(item, n, ty, tx);
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<TO, TQ, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
-                                  wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h,
-                                  headw_s, headb_s);
+        conv_epilogue<TO, TQ, TP, EPI, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
+                                           tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s, headb_s);
 #pragma unroll
       for (int t = 0; t < TC; ++t)
 #pragma unroll
@@ -827,6 +1189,21 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
       ++item;
     }
   }
+}
+
+template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ>
+static hipError_t launch_ring8(const IgemmArgs& a, hipStream_t s) {
+  using G = Ring8Geom<T, TCW, NS, TPS, WST>;
+  if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + G::TW - 1) / G::TW) return hipErrorInvalidValue;
+  if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
+  if (WST && (9 / TPS) * (a.Cin / G::BKE) > G::WST_STEPS) return hipErrorInvalidValue;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  int n_slots = kNumCUs / a.n_ct;   // one 512-thread block per CU
+  if (n_slots < 1) n_slots = 1;
+  if (n_slots > n_mt) n_slots = n_mt;
+  hipLaunchKernelGGL((conv3x3_ring8_kernel<T, TCW, NS, EPI, TPS, WST, TO, TQ>), dim3(a.n_ct * n_slots), dim3(512), 0,
+                     s, a);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------
@@ -1025,7 +1402,6 @@ __global__ __launch_bounds__(256) void first_conv_kernel(const FirstConvArgs a) 
 // (bias + ReLU, 16-byte NHWC stores): the kernel is bound by the output write.
 template <typename T, int C>
 __global__ __launch_bounds__(256) void first_conv_mfma_kernel(const FirstConvArgs a, const IgemmArgs e) {
-  constexpr int KW = 9 * C;
   __shared__ float xs[C * 18 * 18];
   __shared__ float bias_s[64];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1042,18 +1418,22 @@ __global__ __launch_bounds__(256) void first_conv_mfma_kernel(const FirstConvArg
     xs[i] = ok ? a.x[(((long long)n * C + c) * H + iy) * W + ix] : 0.f;
   }
   if (tid < 64) bias_s[tid] = a.b[tid];
-  // A fragments (weights): row t*16 + (lane&15), k = 8*(lane>>4) .. +7
+  // Three 16x16x16 MFMAs per 16 pixels x 16 channels with K slot 4q + c of MFMA m = (tap 4m + q,
+  // channel c): the K order of the ring kernel's fused first conv, so both paths agree bitwise.
+  // A fragments (weights, a.wp = [t][m][16 rows][16 k]): row t*16 + (lane&15), k = 4q .. 4q+3
   const int q = lane >> 4, col = lane & 15;
-  uint4 af[4];
+  uint2 af[4][3];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
-    af[t] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.wp) + ((t * 16 + col) * 32 + 8 * q) * sizeof(T));
-  int koff[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 8 * q + j;
-    const int c = k / 9, r = k - (k / 9) * 9;
-    koff[j] = k < KW ? c * 324 + (r / 3) * 18 + (r - (r / 3) * 3) : -1;
+    for (int m = 0; m < 3; ++m)
+      af[t][m] = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(a.wp) +
+                                                 (((t * 3 + m) * 16 + col) * 16 + 4 * q) * sizeof(T));
+  int toff[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int tp = 4 * m + q;
+    toff[m] = tp < 9 ? (tp / 3) * 18 + (tp - (tp / 3) * 3) : -1;
   }
   __syncthreads();
   f32x4 acc[4][4];
@@ -1062,21 +1442,20 @@ __global__ __launch_bounds__(256) void first_conv_mfma_kernel(const FirstConvArg
     int py, px;
     pix_of((wave * 4 + p) * 16 + col, py, px);
     const int base = py * 18 + px;
-    float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = koff[j] >= 0 ? xs[base + koff[j]] : 0.f;
-    uint4 bf;
-    if constexpr (sizeof(T) == 2) {
-      typedef T t8 __attribute__((ext_vector_type(8)));
-      t8 h;
+    for (int t = 0; t < 4; ++t) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) h[j] = (T)v[j];
-      bf = __builtin_bit_cast(uint4, h);
-    }
+    for (int m = 0; m < 3; ++m) {
+      uint2 bv = uint2{0u, 0u};
+      if constexpr (sizeof(T) == 2) {
+        typedef T t4 __attribute__((ext_vector_type(4)));
+        t4 h;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_frag<T>(acc[t][p], af[t], bf);
+        for (int c = 0; c < 4; ++c) h[c] = (T)(c < C && toff[m] >= 0 ? xs[c * 324 + base + toff[m]] : 0.f);
+        bv = __builtin_bit_cast(uint2, h);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t][p] = mfma16<T>(af[t][m], bv, acc[t][p]);
     }
   }
   conv_epilogue<T, T, 4, EPI_STORE>(e, acc, n, ty * 16, tx * 16, wave * 4, 0, bias_s, nullptr, nullptr);
@@ -1097,7 +1476,7 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ>
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ, int ABL = 0>
 static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
   using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS>;
   if constexpr (HS != 0) {
@@ -1110,6 +1489,13 @@ static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
   int n_slots = (kNumCUs * per_cu) / a.n_ct;
   if (n_slots < 1) n_slots = 1;
   if (n_slots > n_mt) n_slots = n_mt;
+#ifdef UNET_ABLATION
+  if constexpr (ABL != 0) {
+    hipLaunchKernelGGL((conv3x3_ring_abl_kernel<T, WR, WPX, TCW, NS, EPI, TPS, HS, TO, TQ, ABL>), dim3(a.n_ct * n_slots),
+                       dim3(64 * WR * WPX), 0, s, a);
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL((conv3x3_ring_kernel<T, WR, WPX, TCW, NS, EPI, TPS, HS, TO, TQ>), dim3(a.n_ct * n_slots),
                      dim3(64 * WR * WPX), 0, s, a);
   return hipGetLastError();
@@ -1130,10 +1516,21 @@ static hipError_t launch_tring(const IgemmArgs& a, hipStream_t s) {
 
 // 3x3 layers.  T = operand type, TO / TQ = output / pooled-map types (the LDS-halo family runs
 // only with TO = TQ = T: it is the fp32 path).
-template <typename T, typename TO, typename TQ, int EPI>
+template <typename T, typename TO, typename TQ, int EPI, int ABL = 0>
 static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
   constexpr bool same = std::is_same<T, TO>::value && std::is_same<TO, TQ>::value;
   if (EPI == EPI_HEAD && cfg_rows(cfg) != 64) return hipErrorInvalidValue;   // the head needs all 64 channels
+  if constexpr (ABL != 0) {   // ablation builds: the ring configurations only
+    switch (cfg) {
+      case CFG_RING_R128: if constexpr (EPI != EPI_HEAD) return launch_ring<T, 1, 4, 8, 3, EPI, 1, 0, TO, TQ, ABL>(a, s); break;
+      case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 3, 0, TO, TQ, ABL>(a, s);
+      case CFG_RING_FUSED_IN:
+        if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ, ABL>(a, s);
+        break;
+      default: break;
+    }
+    return hipErrorInvalidValue;
+  }
   switch (cfg) {
     case CFG_HALO_R64_W4: if constexpr (same) return launch_halo<T, 1, 4, 4, 3, EPI, 3>(a, s); break;
     case CFG_HALO_R64_W8: if constexpr (same) return launch_halo<T, 1, 8, 4, 3, EPI, 3>(a, s); break;
@@ -1143,6 +1540,9 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
     case CFG_RING_FUSED_IN:
       if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
       break;
+    case CFG_RING8_R128: if constexpr (EPI != EPI_HEAD) return launch_ring8<T, 8, 4, EPI, 1, 0, TO, TQ>(a, s); break;
+    case CFG_RING8_R64_T3: return launch_ring8<T, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
+    case CFG_RING8_R64_WS: return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
     default: break;
   }
   return hipErrorInvalidValue;
@@ -1164,6 +1564,24 @@ static hipError_t launch_up(int cfg, const IgemmArgs& a, hipStream_t s) {
 
 template <typename T, typename TO, typename TQ>
 static hipError_t launch_typed(int cfg, int taps, int epi, const IgemmArgs& a, hipStream_t s) {
+#ifdef UNET_ABLATION
+  if (taps == 9 && cfg >= CFG_COUNT) {   // cfg = base + 16 * ablation (csrc/unet_kernels.hip ring_body)
+    const int base = cfg % 16;
+#define UNET_ABL_CASE(k)                                                             \
+  case k:                                                                            \
+    switch (epi) {                                                                   \
+      case EPI_STORE: return launch_3x3<T, TO, TQ, EPI_STORE, k>(base, a, s);       \
+      case EPI_POOL: return launch_3x3<T, TO, TQ, EPI_POOL, k>(base, a, s);         \
+      case EPI_HEAD: return launch_3x3<T, TO, TQ, EPI_HEAD, k>(base, a, s);         \
+      default: return hipErrorInvalidValue;                                          \
+    }
+    switch (cfg / 16) {
+      UNET_ABL_CASE(1) UNET_ABL_CASE(2) UNET_ABL_CASE(3) UNET_ABL_CASE(4) UNET_ABL_CASE(5)
+      default: return hipErrorInvalidValue;
+    }
+#undef UNET_ABL_CASE
+  }
+#endif
   if (taps == 9) {
     switch (epi) {
       case EPI_STORE: return launch_3x3<T, TO, TQ, EPI_STORE>(cfg, a, s);
@@ -1188,7 +1606,7 @@ hipError_t launch_igemm(DType t, DType to, DType tq, int cfg, int taps, int epi,
   // the mixed bf16 / fp16 plan's two seams (unet_capi.cpp): an fp16 pooled layer whose pooled map
   // feeds a bf16 layer, and a bf16 ConvTranspose whose output feeds an fp16 layer
   if (t == DType::F16 && to == DType::F16 && tq == DType::BF16 && taps == 9 && epi == EPI_POOL)
-    return launch_3x3<_Float16, _Float16, __bf16, EPI_POOL>(cfg, a, s);
+    return launch_typed<_Float16, _Float16, __bf16>(cfg, taps, epi, a, s);
   if (t == DType::BF16 && to == DType::F16 && tq == DType::F16 && taps == 1 && epi == EPI_UPSCATTER)
     return launch_up<__bf16, _Float16>(cfg, a, s);
   return hipErrorInvalidValue;

@@ -23,6 +23,7 @@ UNET_OK, UNET_EINVAL, UNET_ESHAPE, UNET_ENOMEM, UNET_EHIP, UNET_ESTATE, UNET_EKE
 DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16": 2, "mixed": 3}
 MASK_NONE, MASK_U8, MASK_BITS = 0, 1, 2
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
+COMM_ID_BYTES = 128
 IN_F32, IN_U8 = 0, 1
 
 # every function include/unet_mi355x.h declares: name -> (restype, argtypes)
@@ -54,6 +55,10 @@ SIGNATURES = {
     "unet_graph_create": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _i, ctypes.POINTER(_vp)]),
     "unet_graph_launch": (_i, [_vp, _vp]),
     "unet_graph_destroy": (_i, [_vp]),
+    "unet_comm_get_unique_id": (_i, [_vp]),
+    "unet_comm_init": (_i, [_vp, _i, _i, _vp]),
+    "unet_allgather": (_i, [_vp, _vp, _vp, _sz, _vp]),
+    "unet_comm_destroy": (_i, [_vp]),
     "unet_destroy": (_i, [_vp]),
     "unet_last_error": (ctypes.c_char_p, []),
     "unet_abi_version": (_i, []),
@@ -218,6 +223,30 @@ class Handle:
         gr = Graph(self, g, (x, logits, masks, boxes))
         self._graphs.add(gr)
         return gr
+
+    # ---- multi-GPU extras (include/unet_mi355x.h): RCCL all-gather for a host without torch.distributed
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        check(load_library().unet_comm_get_unique_id(buf), "unet_comm_get_unique_id")
+        return buf.raw
+
+    def comm_init(self, rank: int, nranks: int, uid: bytes) -> None:
+        buf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        with self.lock:
+            check(self.lib.unet_comm_init(self._h, rank, nranks, buf), "unet_comm_init")
+
+    def allgather(self, send: torch.Tensor, recv: torch.Tensor, stream: int) -> None:
+        """recv[r] = rank r's ``send`` (contiguous device tensors, recv = nranks x send bytes)."""
+        if not (send.is_contiguous() and recv.is_contiguous()):
+            raise ValueError("send and recv must be contiguous")
+        with self.lock:
+            check(self.lib.unet_allgather(self._h, send.data_ptr(), recv.data_ptr(),
+                                          send.numel() * send.element_size(), stream), "unet_allgather")
+
+    def comm_destroy(self) -> None:
+        with self.lock:
+            check(self.lib.unet_comm_destroy(self._h), "unet_comm_destroy")
 
     def launch_labels(self) -> list:
         """Kernel instantiation of every launch of a forward (include/unet_mi355x.h order)."""
