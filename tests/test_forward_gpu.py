@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 TOL = {"fp32": 1e-4, "fp16": 5e-3, "bf16": 3.5e-2, "mixed": 3.5e-2}
 DEV = "cuda:0"
-HALO_CFGS, RING_CFGS, UP_CFGS = [0, 1, 2], [3, 4, 5, 8, 9, 10], [2, 6, 7]   # csrc/unet_internal.h Cfg
+HALO_CFGS, RING_CFGS, UP_CFGS = [0, 1, 2], [3, 4, 5, 8, 9, 10, 11], [2, 6, 7]   # csrc/unet_internal.h Cfg
 
 
 def make_model(sd_np, c, dtype):

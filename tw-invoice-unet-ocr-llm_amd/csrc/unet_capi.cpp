@@ -154,12 +154,14 @@ const int kUpLevel[4] = {4, 3, 2, 1};   // input level of up4..up1
 //   (profiles/tune_r1_ring.txt), 3 taps per step on the 64-channel layers (tune_r1_ring_t3.txt),
 //   down1.0 fused into down1.3 (tune_r1_ring_fused_in.txt).
 //   fp32: the 128-byte LDS-halo kernel (tune_r1.txt).
+//   round 2: the 8-wave 16x32-tile weight-stationary ring on the two Cin = 64 layers at 512^2
+//   (conv1.3 + head -14 %, down1.3 with the fused first conv -4 %: profiles/tune_r2_ring8*.txt).
 const int kRingCfg[17] = {
-    CFG_RING_FUSED_IN,                                  // down1.0 + down1.3 (+pool), fused
+    CFG_RING8_FUSED_IN,                                 // down1.0 + down1.3 (+pool), fused
     CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128,
     CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128,
     CFG_RING_R128, CFG_RING_R128,                       // down2.0 .. conv2.3
-    CFG_RING_R64_T3, CFG_RING_R64_T3};                  // conv1.0, conv1.3 (+head)
+    CFG_RING_R64_T3, CFG_RING8_R64_WS};                 // conv1.0, conv1.3 (+head)
 const int kHaloCfg[17] = {
     CFG_HALO_R64_W8,                                    // down1.3 (+pool)
     CFG_HALO_R128, CFG_HALO_R128, CFG_HALO_R128, CFG_HALO_R64_W4, CFG_HALO_R128, CFG_HALO_R64_W4,
@@ -431,8 +433,9 @@ std::string layer_label(const Layer& L, int epi) {
                   cfg == CFG_TRING_R256 ? 2 : 1, tname(L.dto));
   } else if (cfg_tile_w(cfg) == 32) {
     std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, %d, %d, %d, %d, %d, %s, %s>", tname(L.dt), cfg_rows(cfg) / 16,
-                  ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING8_R64_WS ? 1 : 0, tname(L.dto),
-                  tname(epi == EPI_POOL ? L.dtq : L.dto));
+                  ring_ns(cfg), epi, ring_tps(cfg), (cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN) ? 1 : 0,
+                  tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto));
+    if (cfg == CFG_RING8_FUSED_IN) std::snprintf(buf + std::strlen(buf) - 1, 8, ", 1>");
   } else if (cfg_is_ring(cfg)) {
     std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %s, %s>", tname(L.dt),
                   cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0,
@@ -458,7 +461,7 @@ void build_labels(unet_handle* h) {
   for (int i = 0; i < UNET_NUM_LAUNCHES; ++i) {
     const int id = order[i];
     if (id < 0) {
-      h->labels[i] = h->L[D1B].cfg % 16 == CFG_RING_FUSED_IN ? std::string("x_to_px4_kernel<") + tname(t0) + ">" : buf;
+      h->labels[i] = cfg_fused_in(h->L[D1B].cfg) ? std::string("x_to_px4_kernel<") + tname(t0) + ">" : buf;
       continue;
     }
     if (id >= 100) { h->labels[i] = layer_label(h->U[id - 100], EPI_UPSCATTER); continue; }
@@ -596,7 +599,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     // keep every layer on a configuration it supports, within the same kernel family (the
     // configurations of a family accumulate in the same K order, so they agree bitwise)
     const bool ring = cfg_is_ring(c);
-    if (c % 16 == CFG_RING_FUSED_IN && (i != D1B || f32)) c = L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128;
+    if (cfg_fused_in(c) && (i != D1B || f32)) c = L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128;
     if (c == CFG_RING8_R64_WS && (L.cin != 64 || f32)) c = L.cout == 64 ? CFG_RING8_R64_T3 : CFG_RING8_R128;   // 72 KB of weights max
     if (c == CFG_RING8_R128 && L.cout == 64) c = CFG_RING8_R64_T3;
     if (cfg_rows(c) > L.cout || (i == C1B && cfg_rows(c) != 64))
@@ -770,7 +773,7 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.ldo = ldo; a.out_off = out_off; a.ldo2 = ldo2;
   a.ncls = h->cfg.n_classes;
   a.mask_kind = mask_kind;
-  if (L.cfg % 16 == CFG_RING_FUSED_IN) {
+  if (cfg_fused_in(L.cfg)) {
     a.x0 = x0;
     a.w0p = h->w0r;
     a.b0 = h->b0;
@@ -819,7 +822,7 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   // down1.net.0 (C -> 64): fused into down1.3 on the 16-bit ring path (fed by the pre-cast input),
   // a direct conv otherwise
   const void* x0 = x;
-  if (h->L[D1B].cfg % 16 == CFG_RING_FUSED_IN) {
+  if (cfg_fused_in(h->L[D1B].cfg)) {
     hipError_t e = launch_x_to_px4(h->L[D1B].dt, x, x_layout, x_dtype, N, C, H, W, buf(B.xpx), s);
     if (e != hipSuccess) return fail(UNET_EHIP, std::string("input pre-cast launch: ") + hipGetErrorString(e));
     x0 = buf(B.xpx);

@@ -81,7 +81,8 @@ enum Cfg : int {
   CFG_RING8_R128 = 8,     // 128 rows, one tap per step, 4 weight slots
   CFG_RING8_R64_T3 = 9,   // 64 rows, 3 taps per step, 3 slots
   CFG_RING8_R64_WS = 10,  // 64 rows, 3 taps per step, weight-stationary (Cin = 64)
-  CFG_COUNT = 11
+  CFG_RING8_FUSED_IN = 11,// RING8_R64_WS for down1.3 with down1.0 fused
+  CFG_COUNT = 12
 };
 int cfg_rows(int cfg);
 bool cfg_is_halo(int cfg);
@@ -89,6 +90,7 @@ bool cfg_is_ring(int cfg);   // 64-byte-row ring kernel: step-major packed weigh
 int ring_ns(int cfg);       // ring kernel: weight-ring slots
 int ring_tps(int cfg);      // ring kernel: taps per step
 int cfg_tile_w(int cfg);    // pixel-tile width (16, or 32 for the 8-wave ring)
+bool cfg_fused_in(int cfg); // down1.0 fused into down1.3 (the network input feeds the kernel)
 bool cfg_is_tring(int cfg); // ConvTranspose ring kernel: step-major packed weights
 int cfg_limit();            // valid Cfg values of this build (ablation builds: + 16 * ablation)
 

@@ -43,20 +43,23 @@ bool cfg_is_halo(int cfg) { return cfg == CFG_HALO_R64_W4 || cfg == CFG_HALO_R64
 bool cfg_is_ring(int cfg) {
   cfg %= 16;
   return cfg == CFG_RING_R128 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R128 ||
-         cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS;
+         cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;
 }
 int cfg_tile_w(int cfg) {
   cfg %= 16;
-  return (cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS) ? 32 : 16;
+  return (cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN) ? 32
+                                                                                                               : 16;
 }
+bool cfg_fused_in(int cfg) { return cfg % 16 == CFG_RING_FUSED_IN || cfg % 16 == CFG_RING8_FUSED_IN; }
 int ring_ns(int cfg) { return cfg % 16 == CFG_RING8_R128 ? 4 : 3; }
 int ring_tps(int cfg) {
   cfg %= 16;
-  return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS) ? 3 : 1;
+  return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS ||
+          cfg == CFG_RING8_FUSED_IN) ? 3 : 1;
 }
 int cfg_limit() {
 #ifdef UNET_ABLATION
-  return CFG_COUNT + 16 * 5;
+  return CFG_COUNT + 16 * 6;
 #else
   return CFG_COUNT;
 #endif
@@ -146,6 +149,38 @@ __device__ __forceinline__ void store16<_Float16>(_Float16* dst, const float (&v
   d[1] = __builtin_bit_cast(uint4, hi);
 }
 
+// A 64-channel group of one pixel (128 B in NHWC) leaves the MFMA layout spread over the four
+// lane rows q (16 channels each), so two plain 16-byte stores per lane write 64 scattered
+// 16-byte pieces per instruction.  One v_permlane32_swap per dword pair regroups them: after
+// it, lane row q holds channels 8*perm(q) .. +7 and 32 + 8*perm(q) .. +7 (perm = 0, 16, 8, 24 /
+// 8), so each of the two store instructions writes one contiguous, 64-byte aligned 64-byte run
+// per pixel: 16 full segments per instruction instead of 64 partial ones.  (Time-neutral on
+// MI355X, profiles/tune_r2_stores.txt: the no-store ablation's apparent gain was the higher
+// clock of MFMAs on all-zero operands, not store cost.)  `grp` = channel 0 of the 64-row group.
+__device__ __forceinline__ int swz_store_off(int q) { return 8 * ((q & 1) * 2 + (q >> 1)); }
+template <typename T>
+__device__ __forceinline__ void store64_grouped(T* grp, const float (&v)[16]) {
+  if constexpr (sizeof(T) == 4) {
+    store16<T>(grp + 16 * ((threadIdx.x & 63) >> 4), v);
+  } else {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    t8 lo, hi;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { lo[i] = (T)v[i]; hi[i] = (T)v[8 + i]; }
+    uint4 x = __builtin_bit_cast(uint4, lo), y = __builtin_bit_cast(uint4, hi);
+    uint4 xs, ys;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane32_swap(x[i], y[i], false, false);
+      xs[i] = r[0];
+      ys[i] = r[1];
+    }
+    T* dst = grp + swz_store_off((threadIdx.x & 63) >> 4);
+    *reinterpret_cast<uint4*>(dst) = xs;
+    *reinterpret_cast<uint4*>(dst + 32) = ys;
+  }
+}
+
 // LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4): lane l's bytes land at
 // lds_dst + 16*l.  Issued from inline asm on purpose: hipcc would otherwise treat every
 // later ds_read as aliasing the in-flight DMA and drain vmcnt(0) in front of it, which
@@ -207,7 +242,7 @@ __device__ __forceinline__ float xsum_lane32(float x) {   // x[l] + x[l ^ 32]
 
 // TO: element type of the NHWC output (and of the ConvTranspose scatter), TQ: of the pooled map
 // (the two differ where a layer feeds consumers of different storage type, see unet_capi.cpp).
-template <typename TO, typename TQ, int TP, int EPI, int TW = 16>
+template <typename TO, typename TQ, int TP, int EPI, int TW = 16, int NOSTORE = 0>
 __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0,
                                               int ox0, int g0, int row0, const float* bias_w,
                                               const float* head_w, const float* head_b) {
@@ -241,10 +276,20 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
         if (EPI != EPI_UPSCATTER) x = relu_nan(x);
         v[t * 4 + e] = x;
       }
-    if constexpr (EPI == EPI_STORE || EPI == EPI_POOL) {
+    if constexpr (NOSTORE) {   // ablation builds: the epilogue arithmetic without its stores
+#pragma unroll
+      for (int e = 0; e < 16; ++e) asm volatile("" ::"v"(v[e]));
+      if constexpr (EPI == EPI_POOL) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float o = max_nan(v[e], dpp_f32<0xB1>(v[e]));
+          asm volatile("" ::"v"(max_nan(o, dpp_f32<0x128>(o))));
+        }
+      }
+    } else if constexpr (EPI == EPI_STORE || EPI == EPI_POOL) {
       if (inside) {
-        TO* dst = reinterpret_cast<TO*>(a.out) + ((long long)(n * H + oy) * W + ox) * a.ldo + a.out_off + rbase;
-        store16<TO>(dst, v);
+        TO* grp = reinterpret_cast<TO*>(a.out) + ((long long)(n * H + oy) * W + ox) * a.ldo + a.out_off + row0;
+        store64_grouped<TO>(grp, v);
       }
       if constexpr (EPI == EPI_POOL) {
         float m[16];
@@ -257,19 +302,17 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
         }
         if ((col & 9) == 0 && oy + 1 < H && ox + 1 < W) {
           const int Ho = H >> 1, Wo = W >> 1;
-          TQ* dst = reinterpret_cast<TQ*>(a.out2) +
-                    ((long long)(n * Ho + (oy >> 1)) * Wo + (ox >> 1)) * a.ldo2 + rbase;
-          store16<TQ>(dst, m);
+          TQ* grp = reinterpret_cast<TQ*>(a.out2) + ((long long)(n * Ho + (oy >> 1)) * Wo + (ox >> 1)) * a.ldo2 + row0;
+          store64_grouped<TQ>(grp, m);   // (lane rows q of one column are all anchors or none)
         }
       }
     } else if constexpr (EPI == EPI_UPSCATTER) {
       if (inside) {
-        const int ab = rbase / a.Cout;
-        const int o0 = rbase - ab * a.Cout;
+        const int ab = row0 / a.Cout;   // a 64-row group lies in one (a, b) quadrant (Cout % 64 == 0)
+        const int o0 = row0 - ab * a.Cout;
         const int Y = 2 * oy + (ab >> 1), X = 2 * ox + (ab & 1);
-        TO* dst = reinterpret_cast<TO*>(a.out) +
-                  ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0;
-        store16<TO>(dst, v);
+        TO* grp = reinterpret_cast<TO*>(a.out) + ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0;
+        store64_grouped<TO>(grp, v);
       }
     } else {  // EPI_HEAD: 1x1 conv 64 -> ncls on the fp32 activations, then masks
       // All class dots first (independent FMA chains), then the 4 row-quads of the
@@ -854,7 +897,9 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
     }
   };
 
+  static_assert(SPC >= NS - 1, "a halo issued after an epilogue is first needed after the barrier-only waits");
   int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
+  int wskip = 0;                            // barrier-only waits left after the last epilogue
   for (int g = 0; g < total; ++g) {
     const bool hnext = tap == 0 && hseq + 1 < hseq_end;
     if constexpr (HS == 0 && ABL != 4) {
@@ -879,12 +924,16 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
     // W(g+1) must have landed (and, at a chunk end, the next halo -- issued 8 steps earlier,
     // so older than W(g+1)).  Younger loads may stay in flight: W(g+2 .. g+NS-1) and a halo
     // issued within the last NS-2 steps (this chunk's tap < NS-2).
+    // Right after a tile's epilogue (wskip > 0) everything the next NS-2 steps need was issued
+    // before it and waited for there, so the wait is the barrier alone: a vmcnt wait would also
+    // wait for the epilogue's global stores (vmcnt counts loads and stores in issue order).
     {
       int young = total - 2 - g;
       young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
       const bool hyoung = HS == 0 && wave < HLW && tap < NS - 2 && hseq + 1 < hseq_end;
       if constexpr (ABL == 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // ablation: no barrier
       else if constexpr (ABL == 4) wait_vm_barrier<0>();
+      else if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }
       else ring_wait<TPS * WI, HI, NS - 2>(young, hyoung);
     }
     bool tile_end = false;
@@ -899,17 +948,27 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
     if (tile_end) {
       int n, ty, tx;
       tile_of(item, n, ty, tx);
-      if constexpr (ABL == 5) {   // ablation: no epilogue (keep the accumulators alive)
+      if constexpr (ABL == 6 && EPI != EPI_HEAD) {   // ablation: epilogue arithmetic, no stores
+#pragma unroll
+        for (int h = 0; h < TC / 4; ++h)
+          conv_epilogue<TO, TQ, TP, EPI, 16, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
+                                                tx * 16, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
+                                                bias_s + wr * 16 * TC + 64 * h, headw_s, headb_s);
+      } else if constexpr (ABL == 5) {   // ablation: no epilogue (keep the accumulators alive)
 #pragma unroll
         for (int t = 0; t < TC; ++t)
 #pragma unroll
           for (int p = 0; p < TP; ++p) asm volatile("" ::"v"(acc[t][p]));
       } else {
+        // every load issued so far (the weights of the next NS-2 steps, the next halo) has landed
+        // before the stores go out; the next NS-2 waits are then barriers only (wskip)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<TO, TQ, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
-                                  wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h,
-                                  headw_s, headb_s);
+        for (int h = 0; h < TC / 4; ++h)
+          conv_epilogue<TO, TQ, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
+                                         wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h,
+                                         headw_s, headb_s);
+        wskip = NS - 2;
       }
 #pragma unroll
       for (int t = 0; t < TC; ++t)
@@ -949,7 +1008,7 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
 // Same K order (chunk32-major, tap-minor), fragment layouts and swizzles as the 4-wave ring (the
 // 34-pixel halo row stride is 544 dwords = 32 mod 64 banks, like the 18-pixel one), so the two
 // agree bitwise.
-template <typename T, int TCW, int NS, int TPS, int WST>
+template <typename T, int TCW, int NS, int TPS, int WST, int HS = 0>
 struct Ring8Geom {
   static constexpr int NW = 8, TW = 32, TP = 4;
   static constexpr int TC = TCW;
@@ -958,7 +1017,7 @@ struct Ring8Geom {
   static constexpr int HWD = TW + 2;                  // halo width (34)
   static constexpr int HP = 18 * HWD;                 // halo pixels (612)
   static constexpr int HI = (HP + 16 * NW - 1) / (16 * NW);   // halo DMA instructions per wave (5)
-  static constexpr int HALO_BYTES = HI * NW * 16 * 64;
+  static constexpr int HALO_BYTES = HS ? HP * 64 : HI * NW * 16 * 64;   // HS: computed, exactly HP rows
   static constexpr int WSLOT = BR * 64;               // one tap's weights
   static constexpr int SLOT = TPS * WSLOT;            // one step
   static constexpr int PIECES = SLOT / 1024;          // weight DMA instructions per step (all waves)
@@ -966,7 +1025,10 @@ struct Ring8Geom {
   static constexpr int WBYTES = WST ? WST_STEPS * SLOT : NS * SLOT;
   static constexpr int WOFF = 2 * HALO_BYTES;
   static constexpr int PARAM_OFF = WOFF + WBYTES;
-  static constexpr int LDS_BYTES = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
+  static constexpr int XW = TW + 4;                   // fused first conv: input window 20 x XW, 4 channels
+  static constexpr int XS_OFF = PARAM_OFF + (HS ? BR : BR + kMaxClasses * 64 + kMaxClasses) * 4;
+  static constexpr int XS_BYTES = HS ? 20 * XW * 4 * (int)sizeof(T) : 0;
+  static constexpr int LDS_BYTES = XS_OFF + XS_BYTES;
 };
 
 template <int N>
@@ -985,9 +1047,12 @@ __device__ __forceinline__ void wait_vm_barrier_rt(int n) {
   }
 }
 
-template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ>
+// HS = 1 (down1.3): down1.0 fused in, as in the 4-wave ring (its halo chunks are computed from a
+// 20 x 36 window of the pre-cast input on 16x16x16 MFMAs); needs WST (the loop then has a barrier
+// after every step: the window is re-filled while the halo of the next tile is computed from it).
+template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0>
 __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a) {
-  using G = Ring8Geom<T, TCW, NS, TPS, WST>;
+  using G = Ring8Geom<T, TCW, NS, TPS, WST, HS>;
   constexpr int NW = G::NW, TW = G::TW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
   constexpr int HWD = G::HWD, HP = G::HP, HI = G::HI, HALO_BYTES = G::HALO_BYTES;
   constexpr int WSLOT = G::WSLOT, SLOT = G::SLOT, PIECES = G::PIECES, WOFF = G::WOFF;
@@ -996,6 +1061,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   static_assert(WST || (NS >= 3 && NS <= 4), "weight ring depth");
   static_assert(EPI != EPI_HEAD || BR == 64, "fused head needs the 64 channels in one block");
   static_assert(G::LDS_BYTES <= 160 * 1024, "LDS");
+  static_assert(HS == 0 || (WST && sizeof(T) == 2 && BR == 64 && TPS == 3 && EPI != EPI_HEAD),
+                "fused first conv: weight-stationary 16-bit 64-row ring, 3 taps per step");
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
   float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
   float* headw_s = bias_s + BR;
@@ -1101,8 +1168,92 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   const int wpos = (q ^ ((col >> 1) & 3)) << 4;
   const char* wrow = lds + WOFF + col * 64 + wpos;
 
+  // ---- HS: fused first conv (down1.0) -> halo chunks (see ring_body) ----
+  // window DMA of tile i: thread L < 360 copies input pixels (2*(L%18), +1) of window row L/18
+  auto issue_xs = [&](int i) {
+    if constexpr (HS != 0) {
+      int n, ty, tx;
+      tile_of(i, n, ty, tx);
+      const int L = tid;
+      if (L < 20 * (G::XW / 2)) {   // lanes past the window stay inactive (no LDS write)
+        const int yy = L / (G::XW / 2), seg = L - (L / (G::XW / 2)) * (G::XW / 2);
+        const int iy = ty * 16 + yy - 2, ix = tx * TW + 2 * seg - 2;
+        const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        const char* src = ok ? reinterpret_cast<const char*>(a.x0) + ((long long)(n * H + iy) * W + ix) * 4 * sizeof(T)
+                             : zero;
+        glds16(src, lds + G::XS_OFF + wave * 1024);
+      }
+    }
+  };
+  uint2 w0f[2][2][3];
+  float b0v[2][8];
+  int toff[3];   // byte offset of this lane's tap in the window, per MFMA (-1: zero tap)
+  if constexpr (HS != 0) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+          w0f[cb][t][m] = *reinterpret_cast<const uint2*>(
+              reinterpret_cast<const char*>(a.w0p) + ((((cb * 2 + t) * 3 + m) * 16 + (lane & 15)) * 16 + 4 * (lane >> 4)) * sizeof(T));
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b0v[cb][j] = a.b0[32 * cb + 8 * (lane >> 4) + j];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int tp = 4 * m + (lane >> 4);
+      toff[m] = tp < 9 ? ((tp / 3) * G::XW + (tp - (tp / 3) * 3)) * 4 * (int)sizeof(T) : -1;
+    }
+  }
+  constexpr int HGR = (HP + 15) / 16;                     // 16-pixel groups of the halo
+  constexpr int HIT = (HGR + 2 * NW - 1) / (2 * NW);      // groups per wave and part
+  auto compute_halo = [&](int i, int cb, int hb, int part) {
+    if constexpr (HS != 0) {
+      int n, ty, tx;
+      tile_of(i, n, ty, tx);
+      const char* xs = lds + G::XS_OFF;
+      char* dst = lds + hb * HALO_BYTES;
+      const int qq = lane >> 4;
+#pragma unroll
+      for (int it = 0; it < HIT; ++it) {
+        const int grp = wave + part * NW + it * 2 * NW;
+        if (grp >= HGR) break;   // wave-uniform
+        const int p = grp * 16 + (lane & 15);
+        const bool real = p < HP;
+        const int hy = real ? p / HWD : 0, hx = real ? p - (p / HWD) * HWD : 0;
+        const char* px = xs + (hy * G::XW + hx) * 4 * (int)sizeof(T);
+        f32x4 acc0[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+          uint2 bv = *reinterpret_cast<const uint2*>(px + (toff[m] < 0 ? 0 : toff[m]));
+          if (toff[m] < 0) bv = uint2{0u, 0u};   // 0 x (a NaN input) must stay 0
+#pragma unroll
+          for (int t = 0; t < 2; ++t) acc0[t] = mfma16<T>(w0f[cb][t][m], bv, acc0[t]);
+        }
+        const int iy = ty * 16 + hy - 1, ix = tx * TW + hx - 1;
+        const bool inimg = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        typedef T t8 __attribute__((ext_vector_type(8)));
+        t8 o;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[4 * t + e] = (T)(inimg ? relu_nan(acc0[t][e] + b0v[cb][4 * t + e]) : 0.f);
+        if (real) *reinterpret_cast<uint4*>(dst + p * 64 + ((qq ^ (hx & 3)) << 4)) = __builtin_bit_cast(uint4, o);
+      }
+    }
+  };
+
   // prologue: halo of chunk 0; weights (all steps, or steps 0 .. NS-2); epilogue parameters
-  issue_halo();
+  if constexpr (HS != 0) {
+    issue_xs(0);
+    wait_vm_barrier<0>();
+    compute_halo(0, 0, 0, 0);
+    compute_halo(0, 0, 0, 1);
+  } else {
+    issue_halo();
+  }
   if constexpr (WST) {
     for (int s = 0; s < S; ++s) issue_w_step(s, s);
   } else {
@@ -1145,15 +1296,29 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     }
   };
 
+  static_assert(WST || SPC >= NS - 1, "see ring_body");
+  int wskip = 0;
   int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
   for (int g = 0; g < total; ++g) {
     const bool hnext = tap == 0 && hseq + 1 < hseq_end;
-    if (hnext) issue_halo();
+    if (HS == 0 && hnext) issue_halo();
     if (!WST && g + NS - 1 < total) issue_w();
+    if constexpr (HS != 0) {   // the next tile's window, once this tile's last halo chunk is computed
+      if (c == 0 && tap == 2 && item + 1 < items) issue_xs(item + 1);
+    }
 #pragma unroll
     for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
+    if constexpr (HS != 0) {   // next chunk's halo into the other buffer, in two halves (see ring_body)
+      if (c == 0 && tap < 2) compute_halo(item, 1, (hseq + 1) & 1, tap);
+      else if (c == 1 && tap >= 1 && item + 1 < items) compute_halo(item + 1, 0, (hseq + 1) & 1, tap - 1);
+    }
     const bool chunk_end = tap == SPC - 1;
-    if constexpr (WST) {
+    if constexpr (HS != 0) {
+      // every step: the window re-fill (chunk 0, step 2) must follow the reads of the halo
+      // computation of steps 0-1, the computed chunk must be visible at the chunk end, and the
+      // window must have landed before chunk 1 computes from it (issued a step earlier)
+      wait_vm_barrier<0>();
+    } else if constexpr (WST) {
       // only the halo streams: the next chunk's halo (issued at this chunk's first step) must
       // have landed, and every wave must be done with this chunk's halo before the next issue
       if (chunk_end) wait_vm_barrier<0>();
@@ -1164,7 +1329,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       int young = total - 2 - g;
       young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
       const bool hyoung = tap < NS - 2 && hseq + 1 < hseq_end;
-      wait_vm_barrier_rt(young * wcnt + (hyoung ? HI : 0));
+      if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }   // see ring_body
+      else wait_vm_barrier_rt(young * wcnt + (hyoung ? HI : 0));
     }
     bool tile_end = false;
     if (++tap == SPC) {
@@ -1178,6 +1344,10 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     if (tile_end) {
       int n, ty, tx;
       tile_of(item, n, ty, tx);
+      if (!WST) {   // see ring_body: the next NS-2 waits are barriers only
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wskip = NS - 2;
+      }
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
         conv_epilogue<TO, TQ, TP, EPI, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
@@ -1191,9 +1361,12 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   }
 }
 
-template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ>
+template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0>
 static hipError_t launch_ring8(const IgemmArgs& a, hipStream_t s) {
-  using G = Ring8Geom<T, TCW, NS, TPS, WST>;
+  using G = Ring8Geom<T, TCW, NS, TPS, WST, HS>;
+  if constexpr (HS != 0) {
+    if (a.Cin != 2 * G::BKE || a.c0 < 1 || a.c0 > 3 || !a.x0 || !a.w0p || !a.b0) return hipErrorInvalidValue;
+  }
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + G::TW - 1) / G::TW) return hipErrorInvalidValue;
   if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
   if (WST && (9 / TPS) * (a.Cin / G::BKE) > G::WST_STEPS) return hipErrorInvalidValue;
@@ -1201,8 +1374,8 @@ static hipError_t launch_ring8(const IgemmArgs& a, hipStream_t s) {
   int n_slots = kNumCUs / a.n_ct;   // one 512-thread block per CU
   if (n_slots < 1) n_slots = 1;
   if (n_slots > n_mt) n_slots = n_mt;
-  hipLaunchKernelGGL((conv3x3_ring8_kernel<T, TCW, NS, EPI, TPS, WST, TO, TQ>), dim3(a.n_ct * n_slots), dim3(512), 0,
-                     s, a);
+  hipLaunchKernelGGL((conv3x3_ring8_kernel<T, TCW, NS, EPI, TPS, WST, TO, TQ, HS>), dim3(a.n_ct * n_slots), dim3(512),
+                     0, s, a);
   return hipGetLastError();
 }
 
@@ -1303,7 +1476,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
     if (young == 2) wait_vm_barrier<2 * (WI + BI)>(); else if (young == 1) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
   }
 
-  int c = 0, item = 0;
+  int c = 0, item = 0, wskip = 0;
   for (int g = 0; g < total; ++g) {
     if (g + NS - 1 < total) issue(g + NS - 1);
     const char* As = lds + (g % NS) * SLOT + wrow;
@@ -1328,12 +1501,15 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
     {   // step g+1 landed; steps g+2 .. g+NS-1 (issued) may stay in flight
       int young = total - 2 - g;
       young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
-      if (young == 2) wait_vm_barrier<2 * (WI + BI)>(); else if (young == 1) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
+      if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }   // after an epilogue: see ring_body
+      else if (young == 2) wait_vm_barrier<2 * (WI + BI)>(); else if (young == 1) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
     }
     if (++c == S) {
       c = 0;
       int n, ty, tx;
       tile_of(item, n, ty, tx);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // steps g+2 .. g+NS-1 landed before the stores
+      wskip = NS - 2;
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
         conv_epilogue<TO, TO, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
@@ -1543,6 +1719,9 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
     case CFG_RING8_R128: if constexpr (EPI != EPI_HEAD) return launch_ring8<T, 8, 4, EPI, 1, 0, TO, TQ>(a, s); break;
     case CFG_RING8_R64_T3: return launch_ring8<T, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
     case CFG_RING8_R64_WS: return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
+    case CFG_RING8_FUSED_IN:
+      if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ, 1>(a, s);
+      break;
     default: break;
   }
   return hipErrorInvalidValue;
@@ -1576,7 +1755,7 @@ static hipError_t launch_typed(int cfg, int taps, int epi, const IgemmArgs& a, h
       default: return hipErrorInvalidValue;                                          \
     }
     switch (cfg / 16) {
-      UNET_ABL_CASE(1) UNET_ABL_CASE(2) UNET_ABL_CASE(3) UNET_ABL_CASE(4) UNET_ABL_CASE(5)
+      UNET_ABL_CASE(1) UNET_ABL_CASE(2) UNET_ABL_CASE(3) UNET_ABL_CASE(4) UNET_ABL_CASE(5) UNET_ABL_CASE(6)
       default: return hipErrorInvalidValue;
     }
 #undef UNET_ABL_CASE
