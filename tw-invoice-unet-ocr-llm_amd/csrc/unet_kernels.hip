@@ -994,11 +994,12 @@ __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_
 // ---------------------------------------------------------------------------------
 // 3x3 conv, 8-wave ring over 16 x 32 pixel tiles (one block per CU)
 // ---------------------------------------------------------------------------------
-// Ablations of the 4-wave ring (profiles/tune_r2_ablation.txt) show the L2 -> LDS stream as the
-// limiter of the layers with few output channels: without the in-loop LDS-DMA conv1.0 runs 40 %
-// faster, conv1.3 33 %, the 128-row layers 14-29 %, while dropping the LDS fragment reads or the
-// barriers changes almost nothing.  Per MFMA a 64-row x 256-pixel block tile streams ~100 B of
-// weights + halo into LDS (the weights dominate: they are re-fetched for every pixel tile).
+// Ablations of the 4-wave ring (profiles/tune_r2_ablation.txt) point at the L2 -> LDS stream of
+// the layers with few output channels: without the in-loop LDS-DMA conv1.0 runs 40 % faster,
+// conv1.3 33 %, the 128-row layers 14-29 %, while dropping the LDS fragment reads or the barriers
+// changes almost nothing (the no-epilogue ablations are confounded: their layers then compute on
+// all-zero inputs, which the chip runs at a higher clock).  Per MFMA a 64-row x 256-pixel block
+// tile streams ~100 B of weights + halo into LDS (mostly weights, re-fetched per pixel tile).
 // This variant doubles the pixel tile (16 x 32, 512 pixels, 8 waves = 2 per SIMD of ONE block per
 // CU, 64 pixels per wave as before), so every weight byte feeds twice the MFMAs and the halo
 // overlap shrinks (18x34 / 512 = 1.20 vs 1.27).  WST = 1 (weight-stationary, Cin = 64 layers):
