@@ -9,14 +9,14 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [ "$2" != "skip-tests" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 180 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
   echo tests ok
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
   echo smoke ok
 fi
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 echo bench ok
-timeout -k 10 300 python bench.py --size 1024 --batch 64 --dtype fp16 --steps 3 --cpu-seconds 10 --no-latency \
+timeout -k 10 300 python bench.py --size 1024 --batch 64 --dtype fp16 --steps 5 --warmup 3 --cpu-seconds 10 --no-latency \
     > gpurun_out/bench_${TAG}_cfg5_fp16_1024.json 2> gpurun_out/bench_${TAG}_cfg5.err
 echo bench cfg5 ok
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
