@@ -73,8 +73,10 @@ def main():
         if not os.path.isdir(p):
             continue
         rows = load_pass(p)
+        # the forward's own launches: every unet:: kernel except the pre/post-processing ones
         ours = [(did, v) for did, v in sorted(rows.items())
-                if any(s in v[0] for s in ("igemm", "first_conv", "halo", "ring_kernel", "x_to_px4"))]
+                if v[0].startswith("_ZN4unet") and not any(s in v[0] for s in ("mask_boxes", "resample", "nhwc_to_nchw",
+                                                                                "to_planar", "x_to_nchw"))]
         last = ours[-len(launches):]
         for i, (did, (name, ctr)) in enumerate(last):
             per_launch[i].update(ctr)
