@@ -48,7 +48,7 @@ extern "C" {
 #define UNET_DTYPE_BF16 1
 #define UNET_DTYPE_F16 2
 /* bf16 at resolution levels 2-4, fp16 at the two full-resolution levels 0-1 (where the mask
- * boundaries are decided): the precision plan of the headline benchmark, see DESIGN.md §4 */
+ * boundaries are decided): the precision plan of the headline benchmark, see DESIGN.md §2 */
 #define UNET_DTYPE_MIXED 3
 
 /* input layouts / dtypes accepted by unet_forward */
@@ -140,7 +140,7 @@ int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channel
 int unet_num_launches(void);
 
 /* Kernel instantiation run by launch i of a forward (e.g.
- * "conv3x3_halo_kernel<__bf16, 1, 4, 1, 3, 1>"), spelled like the demangled symbol that
+ * "conv3x3_ring_kernel<__bf16, 1, 4, 8, 3, 0, 1, 0, __bf16, __bf16>"), spelled like the demangled symbol that
  * rocprofv3 reports; "" for a bad index. */
 const char* unet_launch_label(const unet_handle* h, int i);
 
