@@ -432,10 +432,10 @@ std::string layer_label(const Layer& L, int epi) {
     std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, %d, %d, %s>", tname(L.dt), cfg == CFG_TRING_R256 ? 4 : 3,
                   cfg == CFG_TRING_R256 ? 2 : 1, tname(L.dto));
   } else if (cfg_tile_w(cfg) == 32) {
-    std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, %d, %d, %d, %d, %d, %s, %s>", tname(L.dt), cfg_rows(cfg) / 16,
-                  ring_ns(cfg), epi, ring_tps(cfg), (cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN) ? 1 : 0,
-                  tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto));
-    if (cfg == CFG_RING8_FUSED_IN) std::snprintf(buf + std::strlen(buf) - 1, 8, ", 1>");
+    const int wst = cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;   // weight-stationary
+    std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, %d, %d, %d, %d, %d, %s, %s, %d>", tname(L.dt),
+                  cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), wst, tname(L.dto),
+                  tname(epi == EPI_POOL ? L.dtq : L.dto), cfg == CFG_RING8_FUSED_IN ? 1 : 0);
   } else if (cfg_is_ring(cfg)) {
     std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %s, %s>", tname(L.dt),
                   cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0,
@@ -483,6 +483,7 @@ void parse_overrides(const char* ov, int n, int* cfg_out, bool (*ok)(int, int)) 
     if (colon != std::string::npos) {
       const int li = std::atoi(item.substr(0, colon).c_str()), c = std::atoi(item.substr(colon + 1).c_str());
       if (li >= 0 && li < n && c >= 0 && c < cfg_limit() && ok(li, c)) cfg_out[li] = c;
+      else std::fprintf(stderr, "unet_mi355x: ignoring configuration override '%s'\n", item.c_str());
     }
     pos = end + 1;
   }

@@ -59,7 +59,7 @@ int ring_tps(int cfg) {
 }
 int cfg_limit() {
 #ifdef UNET_ABLATION
-  return CFG_COUNT + 16 * 6;
+  return CFG_COUNT + 16 * 8;
 #else
   return CFG_COUNT;
 #endif
@@ -253,7 +253,6 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4;
   const int col = lane & 15;
-  const int rbase = row0 + q * 16;
   float bv[16];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -623,7 +622,9 @@ __device__ __forceinline__ void ring_wait(int nw, bool halo) {
 // TO / TQ: element types of the output / pooled map (default T), see conv_epilogue.
 // ABL (timing-only ablation builds, `make abl`; never in the product library): 1 = no barrier
 // in the loop, 2 = no MFMA, 3 = no fragment reads in the loop, 4 = no DMA in the loop, 5 = no
-// epilogue -- each gives wrong outputs by construction.
+// epilogue, 6 = epilogue arithmetic without the stores -- each gives wrong outputs by
+// construction.  Variant with correct outputs, for A/B timing (launch_3x3): 8 = NS = 4 on the
+// 128-row ring.
 template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ, int ABL>
 __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
   using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS>;
@@ -1699,8 +1700,13 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
   if (EPI == EPI_HEAD && cfg_rows(cfg) != 64) return hipErrorInvalidValue;   // the head needs all 64 channels
   if constexpr (ABL != 0) {   // ablation builds: the ring configurations only
     switch (cfg) {
-      case CFG_RING_R128: if constexpr (EPI != EPI_HEAD) return launch_ring<T, 1, 4, 8, 3, EPI, 1, 0, TO, TQ, ABL>(a, s); break;
-      case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 3, 0, TO, TQ, ABL>(a, s);
+      case CFG_RING_R128:
+        if constexpr (EPI != EPI_HEAD) {
+          if constexpr (ABL == 8) return launch_ring<T, 1, 4, 8, 4, EPI, 1, 0, TO, TQ, 0>(a, s);   // variant: NS = 4
+          else return launch_ring<T, 1, 4, 8, 3, EPI, 1, 0, TO, TQ, ABL>(a, s);
+        }
+        break;
+      case CFG_RING_R64_T3: if constexpr (ABL < 7) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 0, TO, TQ, ABL>(a, s); break;
       case CFG_RING_FUSED_IN:
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ, ABL>(a, s);
         break;
@@ -1757,6 +1763,7 @@ static hipError_t launch_typed(int cfg, int taps, int epi, const IgemmArgs& a, h
     }
     switch (cfg / 16) {
       UNET_ABL_CASE(1) UNET_ABL_CASE(2) UNET_ABL_CASE(3) UNET_ABL_CASE(4) UNET_ABL_CASE(5) UNET_ABL_CASE(6)
+      UNET_ABL_CASE(8)
       default: return hipErrorInvalidValue;
     }
 #undef UNET_ABL_CASE
