@@ -431,15 +431,15 @@ std::string layer_label(const Layer& L, int epi) {
   if (cfg_is_tring(cfg)) {
     std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, %d, %d, %s>", tname(L.dt), cfg == CFG_TRING_R256 ? 4 : 3,
                   cfg == CFG_TRING_R256 ? 2 : 1, tname(L.dto));
-  } else if (cfg_tile_w(cfg) == 32) {
+  } else if (cfg_is_ring8(cfg)) {
     const int wst = cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;   // weight-stationary
     std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, %d, %d, %d, %d, %d, %s, %s, %d>", tname(L.dt),
                   cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), wst, tname(L.dto),
                   tname(epi == EPI_POOL ? L.dtq : L.dto), cfg == CFG_RING8_FUSED_IN ? 1 : 0);
   } else if (cfg_is_ring(cfg)) {
-    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %s, %s>", tname(L.dt),
+    std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %s, %s, %d, %d>", tname(L.dt),
                   cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0,
-                  tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto));
+                  tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto), cfg_tile_h(cfg), cfg_tile_w(cfg));
   } else {
     const int wpx = cfg == CFG_HALO_R64_W8 ? 8 : 4, tc = cfg == CFG_HALO_R128 ? 8 : 4,
               ns = cfg == CFG_HALO_R128 ? 2 : 3;
@@ -603,6 +603,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     if (cfg_fused_in(c) && (i != D1B || f32)) c = L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128;
     if (c == CFG_RING8_R64_WS && (L.cin != 64 || f32)) c = L.cout == 64 ? CFG_RING8_R64_T3 : CFG_RING8_R128;   // 72 KB of weights max
     if (c == CFG_RING8_R128 && L.cout == 64) c = CFG_RING8_R64_T3;
+    if (c == CFG_RING_R64_W12 && f32) c = CFG_RING_R64_T3;   // 16-bit only
     if (cfg_rows(c) > L.cout || (i == C1B && cfg_rows(c) != 64))
       c = ring ? CFG_RING_R64_T3 : CFG_HALO_R64_W8;
     // the LDS-halo family stores its own operand type only: keep it off the mixed plan's seams
@@ -782,7 +783,7 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   }
   for (int i = 0; i < kMaxClasses; ++i) a.thr_logit[i] = h->thr_logit[i];
   a.tiles_x = (W + cfg_tile_w(L.cfg) - 1) / cfg_tile_w(L.cfg);
-  a.tiles_y = (H + 15) / 16;
+  a.tiles_y = (H + cfg_tile_h(L.cfg) - 1) / cfg_tile_h(L.cfg);
   a.n_ct = L.ctot / cfg_rows(L.cfg);
   hipError_t e = launch_igemm(L.dt, L.dto, epi == EPI_POOL ? L.dtq : L.dto, L.cfg, L.taps, epi, a, s);
   if (e != hipSuccess) return fail(UNET_EHIP, std::string("igemm launch: ") + hipGetErrorString(e));

@@ -82,14 +82,19 @@ enum Cfg : int {
   CFG_RING8_R64_T3 = 9,   // 64 rows, 3 taps per step, 3 slots
   CFG_RING8_R64_WS = 10,  // 64 rows, 3 taps per step, weight-stationary (Cin = 64)
   CFG_RING8_FUSED_IN = 11,// RING8_R64_WS for down1.3 with down1.0 fused
-  CFG_COUNT = 12
+  // 4-wave ring over 12x32 pixel tiles, two blocks per CU: 384 pixels per weight step (1.5x the
+  // 16x16 tile's MFMAs per weight byte), one tap per step, 4 weight slots (64-row layers)
+  CFG_RING_R64_W12 = 12,
+  CFG_COUNT = 13
 };
 int cfg_rows(int cfg);
 bool cfg_is_halo(int cfg);
 bool cfg_is_ring(int cfg);   // 64-byte-row ring kernel: step-major packed weights
 int ring_ns(int cfg);       // ring kernel: weight-ring slots
 int ring_tps(int cfg);      // ring kernel: taps per step
-int cfg_tile_w(int cfg);    // pixel-tile width (16, or 32 for the 8-wave ring)
+int cfg_tile_w(int cfg);    // pixel-tile width (16, or 32 for the 8-wave ring and CFG_RING_R64_W12)
+int cfg_tile_h(int cfg);    // pixel-tile height (16, or 12 for CFG_RING_R64_W12)
+bool cfg_is_ring8(int cfg); // the 8-wave ring kernel (conv3x3_ring8_kernel)
 bool cfg_fused_in(int cfg); // down1.0 fused into down1.3 (the network input feeds the kernel)
 bool cfg_is_tring(int cfg); // ConvTranspose ring kernel: step-major packed weights
 int cfg_limit();            // valid Cfg values of this build (ablation builds: + 16 * ablation)

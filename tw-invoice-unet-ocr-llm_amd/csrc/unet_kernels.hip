@@ -43,15 +43,16 @@ bool cfg_is_halo(int cfg) { return cfg == CFG_HALO_R64_W4 || cfg == CFG_HALO_R64
 bool cfg_is_ring(int cfg) {
   cfg %= 16;
   return cfg == CFG_RING_R128 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R128 ||
-         cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;
+         cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN || cfg == CFG_RING_R64_W12;
 }
-int cfg_tile_w(int cfg) {
+bool cfg_is_ring8(int cfg) {
   cfg %= 16;
-  return (cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN) ? 32
-                                                                                                               : 16;
+  return cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;
 }
+int cfg_tile_w(int cfg) { return (cfg_is_ring8(cfg) || cfg % 16 == CFG_RING_R64_W12) ? 32 : 16; }
+int cfg_tile_h(int cfg) { return cfg % 16 == CFG_RING_R64_W12 ? 12 : 16; }
 bool cfg_fused_in(int cfg) { return cfg % 16 == CFG_RING_FUSED_IN || cfg % 16 == CFG_RING8_FUSED_IN; }
-int ring_ns(int cfg) { return cfg % 16 == CFG_RING8_R128 ? 4 : 3; }
+int ring_ns(int cfg) { return (cfg % 16 == CFG_RING8_R128 || cfg % 16 == CFG_RING_R64_W12) ? 4 : 3; }
 int ring_tps(int cfg) {
   cfg %= 16;
   return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS ||
@@ -386,6 +387,48 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// NT consecutive taps of one ring step (no barrier between them) with the fragment reads of tap
+// k+1 issued under the MFMAs of tap k (register double buffering): only the first tap's LDS read
+// latency is exposed.  Without it every tap opened with a full read -> wait -> MFMA bubble,
+// which the partner wave of a SIMD covers only when it is not in the same phase -- never true
+// right after a barrier of the 8-wave ring, whose two waves per SIMD belong to ONE block.
+// hs[k]: halo fragment base of tap k (+ prow[p] per pixel group), ws[k]: weight row base of tap
+// k (+ t * 1 KB per 16-row group).  Same MFMA sequence per accumulator as one tap at a time.
+template <typename T, int TC, int TP, int NT>
+__device__ __forceinline__ void mfma_taps(f32x4 (&acc)[TC][TP], const char* const (&hs)[NT],
+                                          const char* const (&ws)[NT], const int (&prow)[TP]) {
+  constexpr int NR = TC + TP, NM = TC * TP;
+  static_assert(NM % NR == 0, "read / MFMA interleave");
+  frag_t fa[2][TC], fb[2][TP];
+  auto load = [&](int k, int b) {
+#pragma unroll
+    for (int p = 0; p < TP; ++p) fb[b][p] = *reinterpret_cast<const frag_t*>(hs[k] + prow[p]);
+#pragma unroll
+    for (int t = 0; t < TC; ++t) fa[b][t] = *reinterpret_cast<const frag_t*>(ws[k] + t * 16 * 64);
+  };
+  load(0, 0);
+  __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    const int b = k & 1;
+    if (k + 1 < NT) load(k + 1, b ^ 1);
+#pragma unroll
+    for (int t = 0; t < TC; ++t)
+#pragma unroll
+      for (int p = 0; p < TP; ++p)
+        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, fa[b][t]), __builtin_bit_cast(uint4, fb[b][p]));
+    if (k + 1 < NT) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, NM / NR, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    } else {
+      __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+    }
+  }
+}
+
 // Derived geometry / LDS budget of a halo-kernel instantiation (shared with the launcher).
 template <typename T, int WR, int WPX, int TCW, int NS, int KT>
 struct HaloGeom {
@@ -577,20 +620,24 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
 // Blocks are persistent (n_ct row tiles x n_slots walkers, each walking pixel tiles slot,
 // slot + n_slots, ...) so the rings run across tile boundaries and the epilogue of one tile
 // overlaps the loads of the next.
-constexpr int kRingPix = 18 * 18;
-
-template <typename T, int WR, int WPX, int TCW, int NS, int TPS = 1, int HS = 0>
+// TH x TW: the pixel tile (16 x 16; or 12 x 32 for the 64-channel layers at full resolution:
+// 384 pixels per block at two blocks per CU, see CFG_RING_R64_W12).  The halo is (TH+2) x (TW+2)
+// pixels; its row stride (TW+2) * 16 dwords is 32 mod 64 banks for both widths, so the swizzle
+// below stays conflict-free.
+template <typename T, int WR, int WPX, int TCW, int NS, int TPS = 1, int HS = 0, int TH = 16, int TW = 16>
 struct RingGeom {
   static constexpr int NW = WR * WPX;
   static constexpr int TC = TCW;
-  static constexpr int TP = 16 / WPX;               // 16-pixel groups per wave (16 per tile)
+  static constexpr int HWD = TW + 2;                // halo width
+  static constexpr int HP = (TH + 2) * HWD;         // halo pixels
+  static constexpr int TP = TH * TW / 16 / WPX;     // 16-pixel groups per wave
   static constexpr int BR = WR * 16 * TC;
   static constexpr int BKE = 64 / (int)sizeof(T);   // K elements per step (64 bytes)
   static constexpr int RPI = 16;                    // 64-byte rows per LDS-DMA instruction
-  static constexpr int HLW = NW >= 7 ? 7 : (NW >= 3 ? 3 : NW);   // halo loader waves (21 instr.)
-  static constexpr int HI = (kRingPix + RPI * HLW - 1) / (RPI * HLW);
+  static constexpr int HLW = NW >= 7 ? 7 : (NW >= 3 ? 3 : NW);   // halo loader waves (21 instr. at 16 x 16)
+  static constexpr int HI = (HP + RPI * HLW - 1) / (RPI * HLW);
   // HS = 1: the halo is computed (fused first conv), not DMA'd: exactly 18x18 rows
-  static constexpr int HALO_BYTES = HS ? kRingPix * 64 : HI * HLW * RPI * 64;
+  static constexpr int HALO_BYTES = HS ? HP * 64 : HI * HLW * RPI * 64;
   static constexpr int WI = BR / (RPI * NW);
   static constexpr int WSLOT = BR * 64;              // one tap's weights
   static constexpr int SLOT = TPS * WSLOT;           // one ring slot = one step = TPS taps
@@ -625,20 +672,22 @@ __device__ __forceinline__ void ring_wait(int nw, bool halo) {
 // epilogue, 6 = epilogue arithmetic without the stores -- each gives wrong outputs by
 // construction.  Variant with correct outputs, for A/B timing (launch_3x3): 8 = NS = 4 on the
 // 128-row ring.
-template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ, int ABL>
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ, int ABL,
+          int TH = 16, int TW = 16>
 __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
-  using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS>;
+  using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS, TH, TW>;
   constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
   constexpr int HI = G::HI, WI = G::WI, HLW = G::HLW, HALO_BYTES = G::HALO_BYTES, WSLOT = G::WSLOT;
   constexpr int WOFF = G::WOFF, SLOT = G::SLOT;
+  constexpr int HWD = G::HWD, kRingPix = G::HP;
   constexpr int SPC = 9 / TPS;   // steps per 32-channel chunk
   static_assert(TPS == 1 || TPS == 3, "taps per step");
   static_assert(NS >= 3 && NS <= 5, "weight ring depth");
   static_assert(WI >= 1 && BR % (G::RPI * NW) == 0, "weight tile split");
-  static_assert(TP >= 1 && 16 % WPX == 0, "pixel groups per wave");
+  static_assert(TP >= 1 && (TH * TW / 16) % WPX == 0 && TH % 2 == 0 && TW % 8 == 0, "pixel groups per wave");
   static_assert(EPI != EPI_HEAD || BR == 64, "fused head needs the 64 channels in one block");
-  static_assert(HS == 0 || (sizeof(T) == 2 && BR == 64 && NW == 4 && TPS == 3 && EPI != EPI_HEAD),
-                "fused first conv: 16-bit, 64 rows, 3 taps per step");
+  static_assert(HS == 0 || (sizeof(T) == 2 && BR == 64 && NW == 4 && TPS == 3 && EPI != EPI_HEAD && TH == 16 && TW == 16),
+                "fused first conv: 16-bit, 64 rows, 3 taps per step, 16 x 16 tiles");
   static_assert(WR * WPX >= 8 || G::LDS_BYTES <= 160 * 1024 / 2, "two blocks per CU");
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
   float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
@@ -688,21 +737,32 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
   // both sources advance by cursors: the per-lane halo piece pointers are computed once per
   // pixel tile (chunk c then adds 64c bytes; the zero page covers the invalid pieces of every
   // chunk) and the weight source by one step -- no divisions or 64-bit address math per piece.
-  const char* hsrc[HI];
+  // OFF32 (the 12 x 32 tile, 10 pieces per loader lane): 32-bit per-lane offsets from the
+  // (wave-uniform) image base instead of 64-bit pointers, -1 - chk for a zero-page piece -- 10
+  // VGPRs fewer in a kernel at the 256-register limit (launch_ring: one image < 2 GiB)
+  constexpr bool OFF32 = TH != 16 || TW != 16;
+  const char* hsrc[OFF32 ? 1 : HI];
+  int hoff[OFF32 ? HI : 1];
+  const char* hbase = in;
   int hq_i = 0, hq_c = 0, hq_seq = 0;   // (tile, chunk, sequence number) of the next halo issue
   auto halo_tile = [&](int i) {
     int n, ty, tx;
     tile_of(i, n, ty, tx);
-    const long long pix0 = (long long)(n * H + ty * 16) * W + tx * 16;
+    const long long pix0 = (long long)(n * H + ty * TH) * W + tx * TW;
+    if constexpr (OFF32) hbase = in + (long long)n * H * W * a.ldi * (long long)sizeof(T);
 #pragma unroll
     for (int j = 0; j < HI; ++j) {
       const int row = (wave * HI + j) * 16 + (lane >> 2);
-      const int hy = row / 18, hx = row - (row / 18) * 18;
-      const int iy = ty * 16 + hy - 1, ix = tx * 16 + hx - 1;
+      const int hy = row / HWD, hx = row - (row / HWD) * HWD;
+      const int iy = ty * TH + hy - 1, ix = tx * TW + hx - 1;
       const bool ok = row < kRingPix && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       const int chk = ((lane & 3) ^ (hx & 3)) << 4;
-      const long long pix = pix0 + (long long)(hy - 1) * W + (hx - 1);
-      hsrc[j] = ok ? in + pix * a.ldi * (long long)sizeof(T) + chk : zero + chk;
+      if constexpr (OFF32) {
+        hoff[j] = ok ? (iy * W + ix) * a.ldi * (int)sizeof(T) + chk : -1 - chk;
+      } else {
+        const long long pix = pix0 + (long long)(hy - 1) * W + (hx - 1);
+        hsrc[j] = ok ? in + pix * a.ldi * (long long)sizeof(T) + chk : zero + chk;
+      }
     }
   };
   auto issue_halo = [&]() {   // the next chunk in sequence
@@ -710,7 +770,14 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
       if (hq_c == 0) halo_tile(hq_i);
       char* dst = lds + (hq_seq & 1) * HALO_BYTES + wave * HI * 1024;
 #pragma unroll
-      for (int j = 0; j < HI; ++j) glds16(hsrc[j] + hq_c * 64, dst + j * 1024);
+      for (int j = 0; j < HI; ++j) {
+        if constexpr (OFF32) {
+          const char* src = hoff[j] >= 0 ? hbase + hoff[j] : zero + (-1 - hoff[j]);
+          glds16(src + hq_c * 64, dst + j * 1024);
+        } else {
+          glds16(hsrc[j] + hq_c * 64, dst + j * 1024);
+        }
+      }
     }
     ++hq_seq;
     if (++hq_c == nch) { hq_c = 0; ++hq_i; }
@@ -738,8 +805,8 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
 #pragma unroll
   for (int p = 0; p < TP; ++p) {
     int py, px;
-    pix_of((wp * TP + p) * 16 + col, py, px);
-    prow[p] = (py * 18 + px) * 64;
+    pix_of_w<TW>((wp * TP + p) * 16 + col, py, px);
+    prow[p] = (py * HWD + px) * 64;
   }
   const int px_lane = col & 7;
   const int wpos = (q ^ ((col >> 1) & 3)) << 4;
@@ -863,7 +930,7 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
   }
   auto step = [&](int g, int hs, int tp, int tsub) {
     const int dy = tp / 3, dx = tp - (tp / 3) * 3;
-    const char* Hs = lds + (hs & 1) * HALO_BYTES + (dy * 18 + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
+    const char* Hs = lds + (hs & 1) * HALO_BYTES + (dy * HWD + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
     const char* Ws = wrow + (g % NS) * SLOT + tsub * WSLOT;
     frag_t bq[TP], ar[3];
     if constexpr (ABL == 3) {   // ablation: fragments from registers only
@@ -914,8 +981,19 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
       // is the one that retires it: chunk 1 computes the next tile's halo at its steps 1 and 2.
       if (c == 0 && tap == 2 && item + 1 < items) issue_xs(item + 1);
     }
+    if constexpr (TPS == 3 && ABL == 0 && TC * TP % (TC + TP) == 0) {
+      const char* hs3[3];
+      const char* ws3[3];
 #pragma unroll
-    for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
+      for (int t = 0; t < 3; ++t) {   // taps (dy = tap, dx = t): one kernel row
+        hs3[t] = lds + (hseq & 1) * HALO_BYTES + (tap * HWD + t) * 64 + ((q ^ ((px_lane + t) & 3)) << 4);
+        ws3[t] = wrow + (g % NS) * SLOT + t * WSLOT;
+      }
+      mfma_taps<T, TC, TP, 3>(acc, hs3, ws3, prow);
+    } else {
+#pragma unroll
+      for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
+    }
     if constexpr (HS != 0) {   // next chunk's halo into the other buffer (last read a chunk ago),
       // in two halves: chunk 1 of this tile at steps 0, 1 of chunk 0; chunk 0 of the next tile
       // at steps 1, 2 of chunk 1 (down1.3: Cin = 64, so nch = 2 and SPC = 3)
@@ -952,8 +1030,8 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
       if constexpr (ABL == 6 && EPI != EPI_HEAD) {   // ablation: epilogue arithmetic, no stores
 #pragma unroll
         for (int h = 0; h < TC / 4; ++h)
-          conv_epilogue<TO, TQ, TP, EPI, 16, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
-                                                tx * 16, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
+          conv_epilogue<TO, TQ, TP, EPI, TW, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * TH,
+                                                tx * TW, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
                                                 bias_s + wr * 16 * TC + 64 * h, headw_s, headb_s);
       } else if constexpr (ABL == 5) {   // ablation: no epilogue (keep the accumulators alive)
 #pragma unroll
@@ -966,9 +1044,9 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int h = 0; h < TC / 4; ++h)
-          conv_epilogue<TO, TQ, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
-                                         wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h,
-                                         headw_s, headb_s);
+          conv_epilogue<TO, TQ, TP, EPI, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * TH,
+                                             tx * TW, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
+                                             bias_s + wr * 16 * TC + 64 * h, headw_s, headb_s);
         wskip = NS - 2;
       }
 #pragma unroll
@@ -981,9 +1059,9 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
 }
 
 template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS = 1, int HS = 0, typename TO = T,
-          typename TQ = TO>
+          typename TQ = TO, int TH = 16, int TW = 16>
 __global__ __launch_bounds__(64 * WR * WPX, WR * WPX >= 8 ? 1 : 2) void conv3x3_ring_kernel(const IgemmArgs a) {
-  ring_body<T, WR, WPX, TCW, NS, EPI, TPS, HS, TO, TQ, 0>(a);
+  ring_body<T, WR, WPX, TCW, NS, EPI, TPS, HS, TO, TQ, 0, TH, TW>(a);
 }
 #ifdef UNET_ABLATION
 template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ, int ABL>
@@ -1308,8 +1386,35 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     if constexpr (HS != 0) {   // the next tile's window, once this tile's last halo chunk is computed
       if (c == 0 && tap == 2 && item + 1 < items) issue_xs(item + 1);
     }
+    if constexpr (WST && HS == 0 && TPS == 3 && TC * TP % (TC + TP) == 0) {
+      // weight-stationary, DMA'd halo: no barrier inside a chunk, so its nine taps (three steps)
+      // run as one pipelined sequence at the chunk's first step; the other two only keep count
+      if (tap == 0) {
+        const int ws0 = g - (g / S) * S;   // first step of the chunk within the tile
+        const char* hs9[9];
+        const char* ws9[9];
 #pragma unroll
-    for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
+        for (int k = 0; k < 9; ++k) {   // tap (dy, dx) = (k / 3, k % 3)
+          const int dy = k / 3, dx = k % 3;
+          hs9[k] = lds + (hseq & 1) * HALO_BYTES + (dy * HWD + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
+          ws9[k] = wrow + (ws0 + dy) * SLOT + dx * WSLOT;
+        }
+        mfma_taps<T, TC, TP, 9>(acc, hs9, ws9, prow);
+      }
+    } else if constexpr (TPS == 3 && TC * TP % (TC + TP) == 0) {
+      const int wslot = WST ? g - (g / S) * S : g % NS;
+      const char* hs3[3];
+      const char* ws3[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {   // taps (dy = tap, dx = t): one kernel row
+        hs3[t] = lds + (hseq & 1) * HALO_BYTES + (tap * HWD + t) * 64 + ((q ^ ((px_lane + t) & 3)) << 4);
+        ws3[t] = wrow + wslot * SLOT + t * WSLOT;
+      }
+      mfma_taps<T, TC, TP, 3>(acc, hs3, ws3, prow);
+    } else {
+#pragma unroll
+      for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
+    }
     if constexpr (HS != 0) {   // next chunk's halo into the other buffer, in two halves (see ring_body)
       if (c == 0 && tap < 2) compute_halo(item, 1, (hseq + 1) & 1, tap);
       else if (c == 1 && tap >= 1 && item + 1 < items) compute_halo(item + 1, 0, (hseq + 1) & 1, tap - 1);
@@ -1654,13 +1759,16 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ, int ABL = 0>
+template <typename T, int WR, int WPX, int TCW, int NS, int EPI, int TPS, int HS, typename TO, typename TQ, int ABL = 0,
+          int TH = 16, int TW = 16>
 static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
-  using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS>;
+  using G = RingGeom<T, WR, WPX, TCW, NS, TPS, HS, TH, TW>;
   if constexpr (HS != 0) {
     if (a.Cin != 2 * G::BKE || a.c0 < 1 || a.c0 > 3 || !a.x0 || !a.w0p || !a.b0) return hipErrorInvalidValue;
   }
-  if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
+  if (a.tiles_y != (a.H + TH - 1) / TH || a.tiles_x != (a.W + TW - 1) / TW) return hipErrorInvalidValue;
+  if ((TH != 16 || TW != 16) && (long long)a.H * a.W * a.ldi * (long long)sizeof(T) >= (1LL << 31))
+    return hipErrorInvalidValue;   // 32-bit halo offsets (ring_body OFF32)
   if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
   constexpr int per_cu = G::NW >= 8 ? 1 : G::BLOCKS_PER_CU;   // 8-wave blocks: registers allow one per CU
@@ -1674,7 +1782,7 @@ static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
     return hipGetLastError();
   }
 #endif
-  hipLaunchKernelGGL((conv3x3_ring_kernel<T, WR, WPX, TCW, NS, EPI, TPS, HS, TO, TQ>), dim3(a.n_ct * n_slots),
+  hipLaunchKernelGGL((conv3x3_ring_kernel<T, WR, WPX, TCW, NS, EPI, TPS, HS, TO, TQ, TH, TW>), dim3(a.n_ct * n_slots),
                      dim3(64 * WR * WPX), 0, s, a);
   return hipGetLastError();
 }
@@ -1720,6 +1828,9 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
     case CFG_HALO_R128: if constexpr (same && EPI != EPI_HEAD) return launch_halo<T, 1, 4, 8, 2, EPI, 3>(a, s); break;
     case CFG_RING_R128: if constexpr (EPI != EPI_HEAD) return launch_ring<T, 1, 4, 8, 3, EPI, 1, 0, TO, TQ>(a, s); break;
     case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
+    case CFG_RING_R64_W12:
+      if constexpr (sizeof(T) == 2) return launch_ring<T, 1, 4, 4, 4, EPI, 1, 0, TO, TQ, 0, 12, 32>(a, s);
+      break;
     case CFG_RING_FUSED_IN:
       if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
       break;
