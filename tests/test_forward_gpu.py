@@ -30,7 +30,7 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 # fp32 6.2e-6, fp16 2.7e-3, bf16 2.1e-2, mixed 1.6e-2, all on the reference's own 512x512 logits)
 TOL = {"fp32": 2e-5, "fp16": 5e-3, "bf16": 3.5e-2, "mixed": 3e-2}
 DEV = "cuda:0"
-HALO_CFGS, RING_CFGS, UP_CFGS = [0, 1, 2], [3, 4, 5, 8, 9, 10, 11, 12], [2, 6, 7]   # csrc/unet_internal.h Cfg
+HALO_CFGS, RING_CFGS, UP_CFGS = [0, 1, 2], [3, 4, 5, 8, 9, 10, 11], [2, 6, 7]   # csrc/unet_internal.h Cfg
 
 
 def make_model(sd_np, c, dtype):

@@ -83,7 +83,8 @@ enum Cfg : int {
   CFG_RING8_R64_WS = 10,  // 64 rows, 3 taps per step, weight-stationary (Cin = 64)
   CFG_RING8_FUSED_IN = 11,// RING8_R64_WS for down1.3 with down1.0 fused
   // 4-wave ring over 12x32 pixel tiles, two blocks per CU: 384 pixels per weight step (1.5x the
-  // 16x16 tile's MFMAs per weight byte), one tap per step, 4 weight slots (64-row layers)
+  // 16x16 tile's MFMAs per weight byte), one tap per step, 4 weight slots (64-row layers).
+  // Rejected on A/B (3x the barriers of the T3 ring): built only in `make abl`
   CFG_RING_R64_W12 = 12,
   CFG_COUNT = 13
 };

@@ -62,7 +62,7 @@ int cfg_limit() {
 #ifdef UNET_ABLATION
   return CFG_COUNT + 16 * 8;
 #else
-  return CFG_COUNT;
+  return CFG_RING_R64_W12;   // the configurations after it are ablation-build only
 #endif
 }
 bool cfg_is_tring(int cfg) { return cfg == CFG_TRING_R128 || cfg == CFG_TRING_R256; }
@@ -1376,6 +1376,61 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     }
   };
 
+  if constexpr (HS != 0) {
+    // Fused first conv (down1.3, Cin = 64: two halo chunks, buffer c for chunk c; weights
+    // stationary).  A tile's 18 taps run as three pipelined 6-tap phases with ONE barrier each
+    // (instead of one per 3-tap step):
+    //   1: chunk 0 rows 0-1 | chunk 1's halo of this tile computed from the window  -> barrier
+    //      (every window read done, so it can be re-filled; chunk 1's halo visible)
+    //   2: chunk 0 row 2 + chunk 1 row 0 | the next tile's window DMA'd           -> vmcnt(0) +
+    //      barrier (window landed; every read of halo buffer 0 done)
+    //   3: chunk 1 rows 1-2 | the next tile's chunk-0 halo computed into buffer 0  -> barrier
+    //      (visible to the next tile's phase 1; every read of buffer 1 done)
+    // Waves w and w + 4 share a SIMD (waves go to SIMDs cyclically): waves 0-3 compute their
+    // share of a halo before the phase's MFMAs, waves 4-7 after them, so on every SIMD one wave's
+    // halo work (window reads, small MFMAs, VALU, LDS writes) runs beside its partner's MFMAs.
+    auto taps6 = [&](int j0) {   // global taps j0 .. j0+5 of the tile: j = 9 * chunk + 3 * row + dx
+      const char* hs6[6];
+      const char* ws6[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int j = j0 + k, ch = j / 9, row = (j % 9) / 3, dx = j % 3;
+        hs6[k] = lds + ch * HALO_BYTES + (row * HWD + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
+        ws6[k] = wrow + (ch * 3 + row) * SLOT + dx * WSLOT;
+      }
+      mfma_taps<T, TC, TP, 6>(acc, hs6, ws6, prow);
+    };
+    auto halo_all = [&](int i, int cb) {   // both halves of chunk cb of tile i -> buffer cb
+      compute_halo(i, cb, cb, 0);
+      compute_halo(i, cb, cb, 1);
+    };
+    const bool early = (wave & 4) == 0;
+    for (int item = 0; item < items; ++item) {
+      const bool more = item + 1 < items;
+      if (early) halo_all(item, 1);
+      taps6(0);
+      if (!early) halo_all(item, 1);
+      wait_vm_barrier<63>();   // barrier only: no load is waited for here
+      if (more) issue_xs(item + 1);
+      taps6(6);
+      wait_vm_barrier<0>();
+      if (more && early) halo_all(item + 1, 0);
+      taps6(12);
+      if (more && !early) halo_all(item + 1, 0);
+      wait_vm_barrier<63>();
+      int n, ty, tx;
+      tile_of(item, n, ty, tx);
+#pragma unroll
+      for (int h = 0; h < TC / 4; ++h)
+        conv_epilogue<TO, TQ, TP, EPI, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
+                                           tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s, headb_s);
+#pragma unroll
+      for (int t = 0; t < TC; ++t)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    return;
+  }
   static_assert(WST || SPC >= NS - 1, "see ring_body");
   int wskip = 0;
   int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
@@ -1383,9 +1438,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     const bool hnext = tap == 0 && hseq + 1 < hseq_end;
     if (HS == 0 && hnext) issue_halo();
     if (!WST && g + NS - 1 < total) issue_w();
-    if constexpr (HS != 0) {   // the next tile's window, once this tile's last halo chunk is computed
-      if (c == 0 && tap == 2 && item + 1 < items) issue_xs(item + 1);
-    }
     if constexpr (WST && HS == 0 && TPS == 3 && TC * TP % (TC + TP) == 0) {
       // weight-stationary, DMA'd halo: no barrier inside a chunk, so its nine taps (three steps)
       // run as one pipelined sequence at the chunk's first step; the other two only keep count
@@ -1415,17 +1467,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 #pragma unroll
       for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
     }
-    if constexpr (HS != 0) {   // next chunk's halo into the other buffer, in two halves (see ring_body)
-      if (c == 0 && tap < 2) compute_halo(item, 1, (hseq + 1) & 1, tap);
-      else if (c == 1 && tap >= 1 && item + 1 < items) compute_halo(item + 1, 0, (hseq + 1) & 1, tap - 1);
-    }
     const bool chunk_end = tap == SPC - 1;
-    if constexpr (HS != 0) {
-      // every step: the window re-fill (chunk 0, step 2) must follow the reads of the halo
-      // computation of steps 0-1, the computed chunk must be visible at the chunk end, and the
-      // window must have landed before chunk 1 computes from it (issued a step earlier)
-      wait_vm_barrier<0>();
-    } else if constexpr (WST) {
+    if constexpr (WST) {
       // only the halo streams: the next chunk's halo (issued at this chunk's first step) must
       // have landed, and every wave must be done with this chunk's halo before the next issue
       if (chunk_end) wait_vm_barrier<0>();
@@ -1828,9 +1871,11 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
     case CFG_HALO_R128: if constexpr (same && EPI != EPI_HEAD) return launch_halo<T, 1, 4, 8, 2, EPI, 3>(a, s); break;
     case CFG_RING_R128: if constexpr (EPI != EPI_HEAD) return launch_ring<T, 1, 4, 8, 3, EPI, 1, 0, TO, TQ>(a, s); break;
     case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
+#ifdef UNET_ABLATION   // rejected on A/B (profiles/tune_r2j_ring_w12_rejected.txt): ablation builds only
     case CFG_RING_R64_W12:
       if constexpr (sizeof(T) == 2) return launch_ring<T, 1, 4, 4, 4, EPI, 1, 0, TO, TQ, 0, 12, 32>(a, s);
       break;
+#endif
     case CFG_RING_FUSED_IN:
       if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
       break;
