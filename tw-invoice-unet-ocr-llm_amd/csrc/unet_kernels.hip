@@ -1107,8 +1107,9 @@ struct Ring8Geom {
   static constexpr int PARAM_OFF = WOFF + WBYTES;
   static constexpr int XW = TW + 4;                   // fused first conv: input window 20 x XW, 4 channels
   static constexpr int XS_OFF = PARAM_OFF + (HS ? BR : BR + kMaxClasses * 64 + kMaxClasses) * 4;
-  static constexpr int XS_BYTES = HS ? 20 * XW * 4 * (int)sizeof(T) : 0;
-  static constexpr int LDS_BYTES = XS_OFF + XS_BYTES;
+  static constexpr int XS1 = 20 * XW * 4 * (int)sizeof(T);   // one input window
+  static constexpr int XS_BYTES = HS ? 2 * XS1 : 0;            // double-buffered (tile i: buffer i & 1)
+  static constexpr int LDS_BYTES = XS_OFF + XS_BYTES;          // HS: exactly 160 KiB
 };
 
 template <int N>
@@ -1250,7 +1251,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 
   // ---- HS: fused first conv (down1.0) -> halo chunks (see ring_body) ----
   // window DMA of tile i: thread L < 360 copies input pixels (2*(L%18), +1) of window row L/18
-  auto issue_xs = [&](int i) {
+  auto issue_xs = [&](int i) {   // -> window buffer i & 1
     if constexpr (HS != 0) {
       int n, ty, tx;
       tile_of(i, n, ty, tx);
@@ -1261,7 +1262,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
         const char* src = ok ? reinterpret_cast<const char*>(a.x0) + ((long long)(n * H + iy) * W + ix) * 4 * sizeof(T)
                              : zero;
-        glds16(src, lds + G::XS_OFF + wave * 1024);
+        glds16(src, lds + G::XS_OFF + (i & 1) * G::XS1 + wave * 1024);
       }
     }
   };
@@ -1293,7 +1294,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     if constexpr (HS != 0) {
       int n, ty, tx;
       tile_of(i, n, ty, tx);
-      const char* xs = lds + G::XS_OFF;
+      const char* xs = lds + G::XS_OFF + (i & 1) * G::XS1;
       char* dst = lds + hb * HALO_BYTES;
       const int qq = lane >> 4;
 #pragma unroll
@@ -1378,46 +1379,42 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 
   if constexpr (HS != 0) {
     // Fused first conv (down1.3, Cin = 64: two halo chunks, buffer c for chunk c; weights
-    // stationary).  A tile's 18 taps run as three pipelined 6-tap phases with ONE barrier each
-    // (instead of one per 3-tap step):
-    //   1: chunk 0 rows 0-1 | chunk 1's halo of this tile computed from the window  -> barrier
-    //      (every window read done, so it can be re-filled; chunk 1's halo visible)
-    //   2: chunk 0 row 2 + chunk 1 row 0 | the next tile's window DMA'd           -> vmcnt(0) +
-    //      barrier (window landed; every read of halo buffer 0 done)
-    //   3: chunk 1 rows 1-2 | the next tile's chunk-0 halo computed into buffer 0  -> barrier
-    //      (visible to the next tile's phase 1; every read of buffer 1 done)
-    // Waves w and w + 4 share a SIMD (waves go to SIMDs cyclically): waves 0-3 compute their
-    // share of a halo before the phase's MFMAs, waves 4-7 after them, so on every SIMD one wave's
-    // halo work (window reads, small MFMAs, VALU, LDS writes) runs beside its partner's MFMAs.
-    auto taps6 = [&](int j0) {   // global taps j0 .. j0+5 of the tile: j = 9 * chunk + 3 * row + dx
-      const char* hs6[6];
-      const char* ws6[6];
+    // stationary; the input window double-buffered, tile i in window i & 1).  A tile's 18 taps
+    // run as two pipelined 9-tap phases (one per chunk) with ONE barrier each (instead of one per
+    // 3-tap step):
+    //   1: the next tile's window DMA'd | chunk 1's halo computed from this tile's window | the
+    //      nine taps of chunk 0  -> vmcnt(0) + barrier (window landed; chunk 1's halo visible;
+    //      every read of halo buffer 0 done)
+    //   2: the next tile's chunk-0 halo computed into buffer 0 | the nine taps of chunk 1
+    //      -> barrier (visible to the next tile's phase 1; every read of buffer 1 done)
+    // A window buffer is re-filled one tile after its last read (two barriers later).  Each wave
+    // computes its share of a halo after the phase's MFMAs (profiles/tune_r2j_fused_phases.txt:
+    // computing it before them on waves 0-3, so that the two waves of a SIMD overlap halo work
+    // with MFMAs, and three 6-tap phases per tile instead of two, were no faster).
+    auto taps9 = [&](int ch) {   // the nine taps of chunk ch (halo buffer ch, weight steps 3ch .. 3ch+2)
+      const char* hs9[9];
+      const char* ws9[9];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const int j = j0 + k, ch = j / 9, row = (j % 9) / 3, dx = j % 3;
-        hs6[k] = lds + ch * HALO_BYTES + (row * HWD + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
-        ws6[k] = wrow + (ch * 3 + row) * SLOT + dx * WSLOT;
+      for (int k = 0; k < 9; ++k) {
+        const int row = k / 3, dx = k % 3;
+        hs9[k] = lds + ch * HALO_BYTES + (row * HWD + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
+        ws9[k] = wrow + (ch * 3 + row) * SLOT + dx * WSLOT;
       }
-      mfma_taps<T, TC, TP, 6>(acc, hs6, ws6, prow);
+      mfma_taps<T, TC, TP, 9>(acc, hs9, ws9, prow);
     };
     auto halo_all = [&](int i, int cb) {   // both halves of chunk cb of tile i -> buffer cb
       compute_halo(i, cb, cb, 0);
       compute_halo(i, cb, cb, 1);
     };
-    const bool early = (wave & 4) == 0;
     for (int item = 0; item < items; ++item) {
       const bool more = item + 1 < items;
-      if (early) halo_all(item, 1);
-      taps6(0);
-      if (!early) halo_all(item, 1);
-      wait_vm_barrier<63>();   // barrier only: no load is waited for here
       if (more) issue_xs(item + 1);
-      taps6(6);
+      taps9(0);
+      halo_all(item, 1);
       wait_vm_barrier<0>();
-      if (more && early) halo_all(item + 1, 0);
-      taps6(12);
-      if (more && !early) halo_all(item + 1, 0);
-      wait_vm_barrier<63>();
+      taps9(1);
+      if (more) halo_all(item + 1, 0);
+      wait_vm_barrier<63>();   // barrier only: no load is waited for here
       int n, ty, tx;
       tile_of(item, n, ty, tx);
 #pragma unroll
