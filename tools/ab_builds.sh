@@ -15,7 +15,7 @@ for b in $BUILDS; do
     first=$b
     UNET_MI355X_LIB=$(lib $b) timeout -k 10 200 python tools/lib_ab.py --save gpurun_out/${TAG}_$b.npz > gpurun_out/${TAG}_ab_$b.txt 2>&1
   else
-    UNET_MI355X_LIB=$(lib $b) timeout -k 10 200 python tools/lib_ab.py --save gpurun_out/${TAG}_$b.npz --compare gpurun_out/${TAG}_$first.npz > gpurun_out/${TAG}_ab_$b.txt 2>&1
+    UNET_MI355X_LIB=$(lib $b) timeout -k 10 200 python tools/lib_ab.py --save gpurun_out/${TAG}_$b.npz --compare gpurun_out/${TAG}_$first.npz > gpurun_out/${TAG}_ab_$b.txt 2>&1 || echo "ab $b: not bitwise (see ${TAG}_ab_$b.txt)"
   fi
   echo "ab $b ok"
 done

@@ -665,13 +665,13 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
     h->w0r = nullptr;
     const DType t0 = h->L[D1B].dt;
     if (t0 != DType::F32) {   // MFMA operand [t][m][16 rows][16 k] (first_conv_mfma_kernel), packed row
-      // rho = 16t + r = natural channel natural_of_packed(rho), k = 4q + c <-> tap 4m + q (< 9), channel c (< C)
+      // rho = 16t + r = natural channel natural_of_packed(rho), k = 4q + c <-> tap first_tap(4m + q) (< 9), channel c (< C)
       std::vector<uint8_t> pk((size_t)4 * 3 * 16 * 16 * 2, 0);
       for (int rho = 0; rho < 64; ++rho) {
         const int o = natural_of_packed(rho), tt = rho >> 4, r = rho & 15;
         for (int m = 0; m < 3; ++m)
           for (int q = 0; q < 4; ++q) {
-            const int tap = 4 * m + q;
+            const int tap = first_tap(4 * m + q);
             if (tap >= 9) continue;
             for (int c = 0; c < C; ++c)
               put_elem(t0, pk, (((size_t)(tt * 3 + m) * 16 + r) * 16 + 4 * q + c), w[(size_t)o * 9 * C + c * 9 + tap]);
@@ -680,7 +680,7 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
       rc = upload(h, &h->w0p, pk.data(), pk.size());
       if (rc) return rc;
       // the ring kernel's fused first conv: [cb][t][m][16 rows][16 k], row (cb, t, r) = channel
-      // 32cb + 8(r>>2) + 4t + (r&3), k = 4q + c <-> tap 4m + q (taps 9..11 zero), channel c (< C)
+      // 32cb + 8(r>>2) + 4t + (r&3), k = 4q + c <-> tap first_tap(4m + q) (15 = zero), channel c (< C)
       std::vector<uint8_t> pr((size_t)2 * 2 * 3 * 16 * 16 * 2, 0);
       for (int cb = 0; cb < 2; ++cb)
         for (int tt = 0; tt < 2; ++tt)
@@ -688,7 +688,7 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
             for (int r = 0; r < 16; ++r) {
               const int o = 32 * cb + 8 * (r >> 2) + 4 * tt + (r & 3);
               for (int q = 0; q < 4; ++q) {
-                const int tap = 4 * m + q;
+                const int tap = first_tap(4 * m + q);
                 if (tap >= 9) continue;
                 for (int c = 0; c < C; ++c)
                   put_elem(t0, pr, ((((size_t)(cb * 2 + tt) * 3 + m) * 16 + r) * 16 + 4 * q + c),

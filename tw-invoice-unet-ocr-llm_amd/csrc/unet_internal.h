@@ -64,6 +64,14 @@ struct FirstConvArgs {
   int N, C, H, W;
 };
 
+// First conv on MFMA (K = 9 taps x 4 channels): K slot 4q + c of MFMA m (m = 0..2, lane group q)
+// holds (tap first_tap(4m + q), channel c); 15 = a zero slot.  The two 32-lane halves of a
+// ds_read_b64 are the lane groups {0, 1} and {2, 3}: each half reads two horizontally adjacent
+// taps (their 16-pixel runs overlap in all but one pixel, which the LDS broadcasts) or one tap and
+// a zero slot that reads the same address (first_tap_addr), so the window reads are conflict-free.
+__host__ __device__ constexpr int first_tap(int s) { return (int)((0xF8F5F2764310ull >> (4 * s)) & 15); }
+__host__ __device__ constexpr int first_tap_addr(int s) { return (int)((0x885522764310ull >> (4 * s)) & 15); }
+
 // Kernel configurations.  The LDS-halo family (128-byte K chunks, one tile per block) is the
 // fp32 path; the 64-byte-row ring family (persistent walkers, double-buffered halo, weight ring;
 // K order chunk32-major / tap-minor) is the 16-bit path; the ConvTranspose ring runs the 2x

@@ -832,8 +832,9 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
   };
   // halo chunk cb (channels 32cb .. 32cb+31 of down1.0's output) of tile i -> halo buffer hb.
   // The first conv runs as three 16x16x16 MFMAs per 16 pixels x 16 channels: K slot 4q + c of
-  // MFMA m is (tap 4m + q, channel c), so lane group q's B operand is ONE 8-byte ds_read_b64 of
-  // the 4-channel window pixel under its tap (taps 9..11 are zero): 3 reads per lane and pixel
+  // MFMA m is (tap first_tap(4m + q), channel c) (unet_internal.h: three slots are zero), so lane
+  // group q's B operand is ONE 8-byte ds_read_b64 of the 4-channel window pixel under its tap,
+  // conflict-free by the choice of the tap order: 3 reads per lane and pixel
   // group instead of 8 scattered 2-byte gathers.  Weights: a.w0p = [cb][t][m][16 rows][16 k].
   uint2 w0f[2][2][3];
   float b0v[2][8];
@@ -853,8 +854,8 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
       for (int j = 0; j < 8; ++j) b0v[cb][j] = a.b0[32 * cb + 8 * (lane >> 4) + j];
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
-      const int tp = 4 * m + (lane >> 4);
-      toff[m] = tp < 9 ? ((tp / 3) * 20 + (tp - (tp / 3) * 3)) * 4 * (int)sizeof(T) : -1;
+      const int ta = first_tap_addr(4 * m + (lane >> 4));   // bit 0: a zero slot
+      toff[m] = ((ta / 3) * 20 + ta % 3) * 4 * (int)sizeof(T) + (first_tap(4 * m + (lane >> 4)) > 8 ? 1 : 0);
     }
   }
   // part = 0 / 1: the even / odd pixel groups of this wave (the chunk is computed over two
@@ -880,8 +881,8 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
         f32x4 acc0[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int m = 0; m < 3; ++m) {
-          uint2 bv = *reinterpret_cast<const uint2*>(px + (toff[m] < 0 ? 0 : toff[m]));
-          if (toff[m] < 0) bv = uint2{0u, 0u};   // 0 x (a NaN input) must stay 0
+          uint2 bv = *reinterpret_cast<const uint2*>(px + (toff[m] & ~1));
+          if (toff[m] & 1) bv = uint2{0u, 0u};   // 0 x (a NaN input) must stay 0
 #pragma unroll
           for (int t = 0; t < 2; ++t) acc0[t] = mfma16<T>(w0f[cb][t][m], bv, acc0[t]);
         }
@@ -1284,8 +1285,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       for (int j = 0; j < 8; ++j) b0v[cb][j] = a.b0[32 * cb + 8 * (lane >> 4) + j];
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
-      const int tp = 4 * m + (lane >> 4);
-      toff[m] = tp < 9 ? ((tp / 3) * G::XW + (tp - (tp / 3) * 3)) * 4 * (int)sizeof(T) : -1;
+      const int ta = first_tap_addr(4 * m + (lane >> 4));   // bit 0: a zero slot
+      toff[m] = ((ta / 3) * G::XW + ta % 3) * 4 * (int)sizeof(T) + (first_tap(4 * m + (lane >> 4)) > 8 ? 1 : 0);
     }
   }
   constexpr int HGR = (HP + 15) / 16;                     // 16-pixel groups of the halo
@@ -1308,8 +1309,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         f32x4 acc0[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int m = 0; m < 3; ++m) {
-          uint2 bv = *reinterpret_cast<const uint2*>(px + (toff[m] < 0 ? 0 : toff[m]));
-          if (toff[m] < 0) bv = uint2{0u, 0u};   // 0 x (a NaN input) must stay 0
+          uint2 bv = *reinterpret_cast<const uint2*>(px + (toff[m] & ~1));
+          if (toff[m] & 1) bv = uint2{0u, 0u};   // 0 x (a NaN input) must stay 0
 #pragma unroll
           for (int t = 0; t < 2; ++t) acc0[t] = mfma16<T>(w0f[cb][t][m], bv, acc0[t]);
         }
@@ -1741,8 +1742,9 @@ __global__ __launch_bounds__(256) void first_conv_mfma_kernel(const FirstConvArg
     xs[i] = ok ? a.x[(((long long)n * C + c) * H + iy) * W + ix] : 0.f;
   }
   if (tid < 64) bias_s[tid] = a.b[tid];
-  // Three 16x16x16 MFMAs per 16 pixels x 16 channels with K slot 4q + c of MFMA m = (tap 4m + q,
-  // channel c): the K order of the ring kernel's fused first conv, so both paths agree bitwise.
+  // Three 16x16x16 MFMAs per 16 pixels x 16 channels with K slot 4q + c of MFMA m = (tap
+  // first_tap(4m + q), channel c): the K order of the ring kernel's fused first conv, so both paths
+  // agree bitwise.
   // A fragments (weights, a.wp = [t][m][16 rows][16 k]): row t*16 + (lane&15), k = 4q .. 4q+3
   const int q = lane >> 4, col = lane & 15;
   uint2 af[4][3];
@@ -1755,8 +1757,8 @@ __global__ __launch_bounds__(256) void first_conv_mfma_kernel(const FirstConvArg
   int toff[3];
 #pragma unroll
   for (int m = 0; m < 3; ++m) {
-    const int tp = 4 * m + q;
-    toff[m] = tp < 9 ? (tp / 3) * 18 + (tp - (tp / 3) * 3) : -1;
+    const int tp = first_tap(4 * m + q);
+    toff[m] = tp < 9 ? (tp / 3) * 18 + tp % 3 : -1;
   }
   __syncthreads();
   f32x4 acc[4][4];
