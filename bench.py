@@ -348,14 +348,25 @@ def main():
         labels = handle.launch_labels()
         ms = handle.forward_timed(x, None, masks, native.MASK_BITS, stream)
         esize = 4 if args.dtype == "fp32" else 2
+        prev = None
         for entry, lab, t in zip(LAUNCHES, labels, ms):
             layer_ms[entry[0]] = round(t, 3)
+            fused = not lab   # a launch slot fused into the previous launch (up1 into conv2.3)
+            if fused:
+                lab = prev
             k = kernels.setdefault(lab, {"launches": 0, "ms": 0.0, "gflop": 0.0, "algo_gb": 0.0, "layers": []})
-            k["launches"] += 1
+            k["launches"] += 0 if fused else 1
             k["ms"] += t
             k["gflop"] += launch_flops(entry, B, S, S, C) / 1e9
-            k["algo_gb"] += launch_bytes(entry, B, S, S, C, esize) / 1e9
+            gb = launch_bytes(entry, B, S, S, C, esize) / 1e9
+            if fused:   # its input is the previous launch's output, never written to HBM: minus both trips
+                _, cin, _, lvl, _ = entry
+                gb -= 2 * B * (S >> lvl) * (S >> lvl) * cin * esize / 1e9
+            k["algo_gb"] += gb
             k["layers"].append(entry[0])
+            if fused:   # issues no dispatch of its own (tools/pmc_summary.py)
+                k.setdefault("fused_layers", []).append(entry[0])
+            prev = lab
         dom_name, dom = max(((n, k) for n, k in kernels.items() if "first_conv" not in n and "x_to_px4" not in n),
                             key=lambda kv: kv[1]["ms"])
         achieved = dom["gflop"] / dom["ms"]   # TFLOP/s (GFLOP / ms)

@@ -60,9 +60,14 @@ def test_golden_logits(path, dtype):
     m.close()
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
 @pytest.mark.parametrize("dtype", ["fp32", "bf16", "mixed"])
-def test_golden_intermediates(dtype):
-    """Per-layer localisation: skips, pools, bottleneck and up-convs vs the reference hooks."""
+def test_golden_intermediates(dtype, fuse, monkeypatch):
+    """Per-layer localisation: skips, pools, bottleneck and up-convs vs the reference hooks.  With
+    up1 fused into conv2.3 (the 16-bit default) conv2.3's output c7 is never stored, and fetching
+    it is an error; UNET_MI355X_FUSE_UP1=0 keeps the two launches."""
+    monkeypatch.setenv("UNET_MI355X_FUSE_UP1", fuse)
+    fused = fuse == "1" and dtype != "fp32"
     z = np.load(os.path.join(GOLD, "unet_c3_h16w16_n3_structured.npz"))
     sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile=str(z["profile"]))
     m = make_model(sd, 3, dtype)
@@ -72,6 +77,10 @@ def test_golden_intermediates(dtype):
     torch.cuda.synchronize()
     for name, key in (("c1", "inter_c1"), ("c2", "inter_c2"), ("c3", "inter_c3"), ("c4", "inter_c4"),
                       ("bn", "inter_bn"), ("u1", "inter_u1_up"), ("u4", "inter_u4_up"), ("c7", "inter_c7")):
+        if name == "c7" and fused:
+            with pytest.raises(RuntimeError, match="not stored"):
+                m.intermediate(name)
+            continue
         ref = z[key]
         got = m.intermediate(name).cpu().numpy().reshape(ref.shape)
         err = rel_err(got, ref)
@@ -419,8 +428,10 @@ def test_every_kernel_config(cfg, monkeypatch):
 
 @pytest.mark.parametrize("cfg", UP_CFGS)
 def test_convtranspose_configs(cfg, monkeypatch):
-    """ConvTranspose2d (up4..up1) on every supported kernel configuration vs the golden."""
+    """ConvTranspose2d (up4..up1) on every supported kernel configuration vs the golden (up1 as
+    its own launch, not fused into conv2.3)."""
     monkeypatch.setenv("UNET_MI355X_UPCFG", ",".join(f"{i}:{cfg}" for i in range(4)))
+    monkeypatch.setenv("UNET_MI355X_FUSE_UP1", "0")
     z = np.load(os.path.join(GOLD, "unet_c3_h16w16_n3_structured.npz"))
     sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile=str(z["profile"]))
     for dtype in ("fp32", "bf16"):
@@ -442,18 +453,27 @@ def _forward_state(m, x):
     with torch.no_grad():
         lg = m(x)
     torch.cuda.synchronize()
-    out = {k: m.intermediate(k).clone() for k in INTER}
+    out = {}
+    for k in INTER:
+        try:
+            out[k] = m.intermediate(k).clone()
+        except RuntimeError:   # c7 with up1 fused into conv2.3: never stored
+            assert k == "c7"
     out["logits"] = lg.clone()
     return out
 
 
 def _first_diff(a, b):
-    return [k for k in INTER + ["logits"] if not torch.equal(a[k], b[k])]
+    assert a.keys() == b.keys()
+    return [k for k in a if not torch.equal(a[k], b[k])]
 
 
 def _forced(cfg, up, sd, x, dtype, monkeypatch):
+    """Configuration families compared unfused: the fused conv2.3 + up1 launch accumulates the
+    ConvTranspose in another K order than the up1 kernel (test_fused_up1_matches_unfused)."""
     monkeypatch.setenv("UNET_MI355X_CFG", ",".join(f"{i}:{cfg}" for i in range(17)) if cfg is not None else "")
     monkeypatch.setenv("UNET_MI355X_UPCFG", ",".join(f"{i}:{up}" for i in range(4)) if up is not None else "")
+    monkeypatch.setenv("UNET_MI355X_FUSE_UP1", "0")
     m = make_model(sd, 3, dtype)
     st = _forward_state(m, x)
     m.close()
@@ -485,12 +505,40 @@ def test_forward_deterministic_and_config_invariant(dtype, monkeypatch):
             d = _first_diff(_forced(cfg, None, sd, x, dtype, monkeypatch), fbase)
             if d:
                 bad.append((cfg, None, d[:3]))
+    ubase = _forced(None, None, sd, x, dtype, monkeypatch)
     for up in UP_CFGS:
-        d = _first_diff(_forced(None, up, sd, x, dtype, monkeypatch), base)
+        d = _first_diff(_forced(None, up, sd, x, dtype, monkeypatch), ubase)
         if d:
             bad.append((None, up, d[:3]))
     print(bad)
     assert bad == []
+
+
+@pytest.mark.parametrize("dtype", ["mixed", "bf16", "fp16"])
+def test_fused_up1_matches_unfused(dtype, monkeypatch):
+    """conv2.3 + up1 in one launch (EPI_UPFUSE, the 16-bit default) vs the two launches: the same
+    products, only the ConvTranspose's fp32 accumulation order differs (its K order follows the
+    conv accumulators' lanes), so u1 agrees to a few 16-bit ulps and the logits / masks agree; the
+    fused run is bitwise repeatable.  Full-size pages (the persistent walker wraps) and a ragged
+    shape (partial tiles at 24 x 40)."""
+    sd = syn.make_state_dict(3, 3, 3, profile="structured")
+    for n, h, w in ((2, 512, 512), (3, 48, 80)):
+        x = torch.from_numpy(syn.invoice_pages(5, n, h, w, 3)).to(DEV)
+        st = {}
+        for fuse in ("1", "0"):
+            monkeypatch.setenv("UNET_MI355X_FUSE_UP1", fuse)
+            m = make_model(sd, 3, dtype)
+            st[fuse] = _forward_state(m, x)
+            if fuse == "1":
+                assert "c7" not in st[fuse]
+                assert _first_diff(_forward_state(m, x), st[fuse]) == []
+            m.close()
+        u_f, u_u = st["1"]["u1"].float(), st["0"]["u1"].float()
+        du = rel_err(u_f.cpu().numpy(), u_u.cpu().numpy())
+        dl = rel_err(st["1"]["logits"].cpu().numpy(), st["0"]["logits"].cpu().numpy())
+        print(f"{dtype} {n}x{h}x{w}: u1 rel diff {du:.2e}, logits rel diff {dl:.2e}")
+        assert du <= (1e-2 if dtype == "bf16" else 2e-3)
+        assert dl <= TOL[dtype]
 
 
 def _np_boxes(masks):

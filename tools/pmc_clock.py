@@ -40,8 +40,12 @@ def main():
     passes = sorted(p for p in glob.glob(os.path.join(a.dir, "pass*")) if os.path.isdir(p))
     per = [load(p) for p in passes]
     # align dispatches of the last forward across passes by order
-    seqs = [[v for k, v in sorted(r.items()) if "unet" in v.get("name", "") and v.get("ms", 0) >= a.min_ms][-21:]
-            for r in per]
+    def last_forward(r):   # the dispatches after the last forward's first launch (input pre-cast / first conv)
+        d = [v for k, v in sorted(r.items()) if "unet" in v.get("name", "")]
+        starts = [i for i, v in enumerate(d) if "x_to_px4" in v["name"] or "first_conv" in v["name"]]
+        d = d[starts[-1] + 1:] if starts else d
+        return [v for v in d if v.get("ms", 0) >= a.min_ms]
+    seqs = [last_forward(r) for r in per]
     print(f"{'#':>3s} {'kernel':44s} {'ms':>7s} {'GHz':>5s} {'mfma%':>6s} {'wait%':>6s} {'winst%':>6s} {'act%':>6s} "
           f"{'L2hit%':>6s} {'ldsconf%':>8s}")
     for i in range(len(seqs[0])):

@@ -67,6 +67,7 @@ def main():
     if a.bench_json:
         kern = json.loads(open(a.bench_json).read().strip().splitlines()[-1])["kernels"]
         fused = {l for k, v in kern.items() if k.startswith("fused_into") for l in v["layers"]}
+        fused |= {l for v in kern.values() for l in v.get("fused_layers", [])}   # e.g. up1 inside conv2.3
         launches = [e for e in LAUNCHES if e[0] not in fused]
     per_launch = [dict() for _ in launches]
     for p in sorted(glob.glob(os.path.join(a.dir, "pass*"))):

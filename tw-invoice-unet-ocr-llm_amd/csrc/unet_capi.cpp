@@ -102,6 +102,12 @@ struct unet_handle {
   float* b0 = nullptr;
   Layer L[17];          // d1b d2a d2b d3a d3b d4a d4b bna bnb c4a c4b c3a c3b c2a c2b c1a c1b
   Layer U[4];           // up4 up3 up2 up1
+  // up1 fused into conv2.3 (EPI_UPFUSE, 16-bit plans): conv2.3's ring weights followed by 8
+  // ConvTranspose steps (pack_fused_up); the forward then has no up1 launch and conv2.3's output
+  // is never stored (unet_debug_fetch "c7" is unavailable).  UNET_MI355X_FUSE_UP1=0 disables it.
+  bool fuse_up1 = false;
+  void* wf_c2b = nullptr;
+  bool last_fused = false;
   float* head_w = nullptr;
   float* head_b = nullptr;
   void* zero = nullptr;
@@ -303,6 +309,36 @@ int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::v
   return rc;
 }
 
+// conv2.3 + up1 (EPI_UPFUSE): conv2.3's ring stream (one 128-row tile, S = 9 * cin / BKE steps,
+// as pack3x3) followed by 8 ConvTranspose steps u = (quadrant u >> 1, K blocks 2 (u & 1) + kbl):
+// slot row 64 kbl + rr = packed row rho = 64 * quadrant + rr (natural row natural_of_packed(rho) =
+// quadrant x 64 + o) of K block kb, K slot 8q + j <-> input channel 64 * (kb >> 1) + 16q + 8 * (kb & 1)
+// + j (the channels each lane of the conv's accumulators holds, ring_body EPI_UPFUSE).
+int pack_fused_up(unet_handle* h, const Layer& L, const Layer& U, const std::vector<double>& w, const float* Wt) {
+  const int BR = 128, BKE = 64 / (int)dtype_size(L.dt), S = 9 * L.cin / BKE;
+  if (L.cout != BR || U.cin != BR || U.cout != 64 || BKE != 32) return fail(UNET_EINVAL, "fused up1: layer shapes");
+  std::vector<uint8_t> buf((size_t)(S + 8) * BR * BKE * dtype_size(L.dt));
+  for (int rho = 0; rho < BR; ++rho) {
+    const int o = natural_of_packed(rho);
+    for (int tap = 0; tap < 9; ++tap)
+      for (int c = 0; c < L.cin; ++c)
+        put_elem(L.dt, buf, ((size_t)((c / BKE) * 9 + tap) * BR + rho) * BKE + c % BKE, w[((size_t)o * L.cin + c) * 9 + tap]);
+  }
+  for (int u = 0; u < 8; ++u) {
+    const int quad = u >> 1, khalf = u & 1;
+    for (int r = 0; r < BR; ++r) {   // slot row r = 64 kbl + rr: quadrant row rr, K block 2 khalf + kbl
+      const int kb = 2 * khalf + (r >> 6);
+      const int nat = natural_of_packed(64 * quad + (r & 63)), ab = nat / 64, o = nat % 64;
+      for (int sl = 0; sl < 32; ++sl) {
+        const int c = 64 * (kb >> 1) + 16 * (sl >> 3) + 8 * (kb & 1) + (sl & 7);
+        put_elem(L.dt, buf, ((size_t)(S + u) * BR + r) * BKE + sl,
+                 Wt[(((size_t)c * U.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]);
+      }
+    }
+  }
+  return upload(h, &h->wf_c2b, buf.data(), buf.size());
+}
+
 // ConvTranspose2d (Cin, Cout, 2, 2) as GEMM rows (a, b, o): packed[rho][c] = W[c][o][a][b]; the
 // ring kernel (cfg_is_tring) takes them in step order per BR-row tile: [ct][c / BKE][BR][BKE].
 int packT(unet_handle* h, Layer& L, const float* W, const float* B) {
@@ -464,8 +500,12 @@ void build_labels(unet_handle* h) {
       h->labels[i] = cfg_fused_in(h->L[D1B].cfg) ? std::string("x_to_px4_kernel<") + tname(t0) + ">" : buf;
       continue;
     }
-    if (id >= 100) { h->labels[i] = layer_label(h->U[id - 100], EPI_UPSCATTER); continue; }
-    const int epi = id == C1B ? EPI_HEAD : (id == D1B || id == D2B || id == D3B || id == D4B) ? EPI_POOL : EPI_STORE;
+    if (id >= 100) {   // a fused up1 launches nothing: empty label (tools: its time and work go to conv2.3)
+      h->labels[i] = (id == 103 && h->fuse_up1) ? std::string() : layer_label(h->U[id - 100], EPI_UPSCATTER);
+      continue;
+    }
+    int epi = id == C1B ? EPI_HEAD : (id == D1B || id == D2B || id == D3B || id == D4B) ? EPI_POOL : EPI_STORE;
+    if (id == C2B && h->fuse_up1) epi = EPI_UPFUSE;
     h->labels[i] = layer_label(h->L[id], epi);
   }
 }
@@ -621,6 +661,11 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     U.dto = U.dtq = level_dtype(cfg->dtype, kUpLevel[i] - 1);
     U.cfg = (ucfgs[i] == CFG_HALO_R128 && U.dto != U.dt) ? (int)CFG_TRING_R256 : ucfgs[i];
   }
+  {
+    const char* fz = std::getenv("UNET_MI355X_FUSE_UP1");
+    const Layer &c2b = h->L[C2B], &u1 = h->U[3];
+    h->fuse_up1 = !(fz && fz[0] == '0') && !f32 && c2b.cfg == CFG_RING_R128 && u1.dt == c2b.dt && u1.dto == c2b.dto;
+  }
   build_labels(h);   // after every layer's configuration (3x3 and ConvTranspose) is final
   DeviceGuard g(cfg->device);
   hipError_t e = hipEventCreateWithFlags(&h->done, hipEventDisableTiming);
@@ -712,6 +757,11 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
     if (!B) return fail(UNET_EKEY, err);
     rc = packT(h, h->U[i], W, B);
     if (rc) return rc;
+    if (i == 3 && h->fuse_up1) {   // conv2.3 + up1 in one launch
+      rc = fold(sd, kLayerKey[C2B][0], kLayerKey[C2B][1], h->L[C2B].cin, h->L[C2B].cout, w, b);
+      if (!rc) rc = pack_fused_up(h, h->L[C2B], h->U[3], w, W);
+      if (rc) return rc;
+    }
   }
   const int ncls = h->cfg.n_classes;
   const float* HW = sd.get("out_conv.weight", {ncls, 64, 1, 1}, err);
@@ -775,6 +825,10 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.ldo = ldo; a.out_off = out_off; a.ldo2 = ldo2;
   a.ncls = h->cfg.n_classes;
   a.mask_kind = mask_kind;
+  if (epi == EPI_UPFUSE) {   // the fused up1's weights, bias and output (the concat buffer's lower half)
+    a.wgt = h->wf_c2b;
+    a.bias2 = h->U[3].b;
+  }
   if (cfg_fused_in(L.cfg)) {
     a.x0 = x0;
     a.w0p = h->w0r;
@@ -868,8 +922,13 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   RUN(h, h->L[C3B], EPI_STORE, buf(B.tA), N, H4, W4, 256, buf(B.tB), 256, 0, nullptr, 0, s);
   RUN(h, h->U[2], EPI_UPSCATTER, buf(B.tB), N, H4, W4, 256, buf(B.cat2), 256, 0, nullptr, 0, s);
   RUN(h, h->L[C2A], EPI_STORE, buf(B.cat2), N, H2, W2, 256, buf(B.tA), 128, 0, nullptr, 0, s);
-  RUN(h, h->L[C2B], EPI_STORE, buf(B.tA), N, H2, W2, 128, buf(B.tB), 128, 0, nullptr, 0, s);
-  RUN(h, h->U[3], EPI_UPSCATTER, buf(B.tB), N, H2, W2, 128, buf(B.cat1), 128, 0, nullptr, 0, s);
+  if (h->fuse_up1) {   // conv2.3 + up1 in one launch (EPI_UPFUSE): up1's slot launches nothing
+    RUN(h, h->L[C2B], EPI_UPFUSE, buf(B.tA), N, H2, W2, 128, nullptr, 0, 0, buf(B.cat1), 128, s);
+    mark();
+  } else {
+    RUN(h, h->L[C2B], EPI_STORE, buf(B.tA), N, H2, W2, 128, buf(B.tB), 128, 0, nullptr, 0, s);
+    RUN(h, h->U[3], EPI_UPSCATTER, buf(B.tB), N, H2, W2, 128, buf(B.cat1), 128, 0, nullptr, 0, s);
+  }
   RUN(h, h->L[C1A], EPI_STORE, buf(B.cat1), N, H, W, 128, buf(B.tA), 64, 0, nullptr, 0, s);
   // conv1.net.3 + BN + ReLU + out_conv (1x1) + sigmoid/threshold, one launch
   RUN(h, h->L[C1B], EPI_HEAD, buf(B.tA), N, H, W, 64, nullptr, 0, 0, nullptr, 0, s,
@@ -883,6 +942,7 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   mark();
   mark_done(h, s);
   h->lastN = N; h->lastH = H; h->lastW = W;
+  h->last_fused = h->fuse_up1;
   return UNET_OK;
 }
 }  // namespace
@@ -1006,6 +1066,9 @@ int unet_debug_fetch(unet_handle* h, const char* name, float* dst, size_t* numel
       {"bn", 8}, {"c7", 9}, {"u1", 10}, {"u2", 11}, {"u3", 12}, {"u4", 13}, {"c8a", 14}};
   auto it = idx.find(name);
   if (it == idx.end()) return fail(UNET_EINVAL, std::string("unknown intermediate ") + name);
+  if (it->second == 9 && h->last_fused)
+    return fail(UNET_ESTATE, "c7 (conv2.3's output) is not stored when up1 is fused into conv2.3 "
+                             "(set UNET_MI355X_FUSE_UP1=0 before creating the handle to keep it)");
   const Src table[] = {{B.cat1, 0, 64, 128, 64},   {B.p1, 1, 64, 64, 0},     {B.cat2, 1, 128, 256, 128},
                        {B.p2, 2, 128, 128, 0},     {B.cat3, 2, 256, 512, 256}, {B.p3, 3, 256, 256, 0},
                        {B.cat4, 3, 512, 1024, 512}, {B.p4, 4, 512, 512, 0},  {B.bnb, 4, 1024, 1024, 0},

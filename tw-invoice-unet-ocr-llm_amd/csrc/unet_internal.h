@@ -16,7 +16,9 @@ enum Epi : int {
   EPI_STORE = 0,    // bias + ReLU -> NHWC store (conv3x3 + folded BN + ReLU)
   EPI_POOL = 1,     // EPI_STORE + fused 2x2/2 max-pool into a second NHWC tensor
   EPI_HEAD = 2,     // bias + ReLU kept in fp32 -> fused 1x1 out_conv -> logits / masks
-  EPI_UPSCATTER = 3 // ConvTranspose2d(k2,s2): bias, no ReLU, pixel-shuffle store
+  EPI_UPSCATTER = 3,// ConvTranspose2d(k2,s2): bias, no ReLU, pixel-shuffle store
+  EPI_UPFUSE = 4    // conv2.3 + up1 in one launch: bias + ReLU kept in registers as the B operand of
+                    // the ConvTranspose2d GEMM (no store), whose output is scattered like EPI_UPSCATTER
 };
 
 // Mask output formats for EPI_HEAD.
@@ -52,6 +54,9 @@ struct IgemmArgs {
   const void* w0p;     // first conv packed [2][2][3][16][16] (unet_capi.cpp, CFG_RING_FUSED_IN)
   const float* b0;     // first conv folded bias [64]
   int c0;              // network input channels (1 or 3)
+  // EPI_UPFUSE: the ConvTranspose2d's bias [4 * Cout / 2] in natural (a, b, o) row order; its
+  // output goes to out2 (pixel stride ldo2, channels [0, Cout / 2)) at 2H x 2W
+  const float* bias2;
 };
 
 struct FirstConvArgs {

@@ -243,10 +243,13 @@ __device__ __forceinline__ float xsum_lane32(float x) {   // x[l] + x[l ^ 32]
 
 // TO: element type of the NHWC output (and of the ConvTranspose scatter), TQ: of the pooled map
 // (the two differ where a layer feeds consumers of different storage type, see unet_capi.cpp).
+// up_out (EPI_UPSCATTER only): scatter into up_out (pixel stride up_ldo, channel offset 0, up_cout
+// channels per (a, b) group) instead of a.out / a.ldo / a.out_off / a.Cout (EPI_UPFUSE).
 template <typename TO, typename TQ, int TP, int EPI, int TW = 16, int NOSTORE = 0>
 __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0,
                                               int ox0, int g0, int row0, const float* bias_w,
-                                              const float* head_w, const float* head_b) {
+                                              const float* head_w, const float* head_b,
+                                              void* up_out = nullptr, int up_ldo = 0, int up_cout = 0) {
   // bias_w: bias of this wave's 64 rows (global or LDS); head_w: [ncls][64] with the
   // wave's 64 rows at +0 (EPI_HEAD only, single 64-row tile); head_b: [ncls]
   constexpr int TC = 4;
@@ -308,10 +311,12 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
       }
     } else if constexpr (EPI == EPI_UPSCATTER) {
       if (inside) {
-        const int ab = row0 / a.Cout;   // a 64-row group lies in one (a, b) quadrant (Cout % 64 == 0)
-        const int o0 = row0 - ab * a.Cout;
+        const int cout = up_out ? up_cout : a.Cout;
+        const int ab = row0 / cout;   // a 64-row group lies in one (a, b) quadrant (Cout % 64 == 0)
+        const int o0 = row0 - ab * cout;
         const int Y = 2 * oy + (ab >> 1), X = 2 * ox + (ab & 1);
-        TO* grp = reinterpret_cast<TO*>(a.out) + ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0;
+        TO* grp = up_out ? reinterpret_cast<TO*>(up_out) + ((long long)(n * 2 * H + Y) * (2 * W) + X) * up_ldo + o0
+                         : reinterpret_cast<TO*>(a.out) + ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0;
         store64_grouped<TO>(grp, v);
       }
     } else {  // EPI_HEAD: 1x1 conv 64 -> ncls on the fp32 activations, then masks
@@ -689,6 +694,12 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
   static_assert(HS == 0 || (sizeof(T) == 2 && BR == 64 && NW == 4 && TPS == 3 && EPI != EPI_HEAD && TH == 16 && TW == 16),
                 "fused first conv: 16-bit, 64 rows, 3 taps per step, 16 x 16 tiles");
   static_assert(WR * WPX >= 8 || G::LDS_BYTES <= 160 * 1024 / 2, "two blocks per CU");
+  // EPI_UPFUSE (conv2.3 + up1): after a tile's S conv steps, SU = 8 more ring steps run the
+  // ConvTranspose2d (K = the 128 conv outputs, rows = 4 quadrants x 64) on the tile's pixels.
+  constexpr bool UPF = EPI == EPI_UPFUSE;
+  static_assert(!UPF || (sizeof(T) == 2 && WR == 1 && WPX == 4 && TC == 8 && TPS == 1 && HS == 0 && TH == 16 && TW == 16),
+                "fused ConvTranspose: the 16-bit 128-row ring (all 128 channels of a pixel in one block)");
+  constexpr int SU = UPF ? 8 : 0;
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
   float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
   float* headw_s = bias_s + BR;
@@ -715,13 +726,14 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
 
   const int H = a.H, W = a.W;
   const int nch = a.Cin / BKE;
-  const int S = SPC * nch;
-  const int total = items * S;
+  const int S = SPC * nch;       // conv steps per tile
+  const int ST = S + SU;         // ring steps per tile
+  const int total = items * ST;
   const int hseq_end = items * nch;
 
   // weights of row tile ct in step order: step s at wblk + s * WSLOT; per lane one 16-byte
   // chunk of row (wave*WI + j)*16 + lane/4, stored at position lane&3 = chunk ^ ((row>>1)&3)
-  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * SLOT +
+  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * ST * SLOT +
                      (wave * WI * 16 + (lane >> 2)) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
   const char* in = reinterpret_cast<const char*>(a.in);
   const char* zero = reinterpret_cast<const char*>(a.zero);
@@ -737,10 +749,10 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
   // both sources advance by cursors: the per-lane halo piece pointers are computed once per
   // pixel tile (chunk c then adds 64c bytes; the zero page covers the invalid pieces of every
   // chunk) and the weight source by one step -- no divisions or 64-bit address math per piece.
-  // OFF32 (the 12 x 32 tile, 10 pieces per loader lane): 32-bit per-lane offsets from the
+  // OFF32 (the 12 x 32 tile, 10 pieces per loader lane; EPI_UPFUSE): 32-bit per-lane offsets from the
   // (wave-uniform) image base instead of 64-bit pointers, -1 - chk for a zero-page piece -- 10
   // VGPRs fewer in a kernel at the 256-register limit (launch_ring: one image < 2 GiB)
-  constexpr bool OFF32 = TH != 16 || TW != 16;
+  constexpr bool OFF32 = TH != 16 || TW != 16 || UPF;
   const char* hsrc[OFF32 ? 1 : HI];
   int hoff[OFF32 ? HI : 1];
   const char* hbase = in;
@@ -790,7 +802,7 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
     for (int t = 0; t < TPS; ++t)
 #pragma unroll
       for (int j = 0; j < WI; ++j) glds16(src + t * WSLOT + j * 1024, dst + t * WSLOT + j * 1024);
-    if (++wq_s == S) wq_s = 0;
+    if (++wq_s == ST) wq_s = 0;
     if (++wq_slot == NS) wq_slot = 0;
   };
 
@@ -966,6 +978,59 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
     }
   };
 
+  // EPI_UPFUSE: the tile's conv outputs relu(acc + bias) as 16-bit B fragments of the
+  // ConvTranspose GEMM.  Lane (pixel col, q) holds natural channels 64h + 16q + 0..15 of its pixels
+  // (the row permutation of the packed weights), so K block kb = 2h + half takes channels
+  // 64h + 16q + 8half + 0..7 in K slots 8q .. 8q+7: every lane's fragment is its own 8 values (the
+  // ConvTranspose weights are packed in this K order, unet_capi.cpp pack_fused_up).  A ConvTranspose
+  // step u = (quadrant u >> 1, K blocks 2 (u & 1) and 2 (u & 1) + 1) streams 64 rows x 64 K of
+  // weights through the ring (slot row 64 kbl + r); a quadrant's 64 x 64-pixel accumulators reuse
+  // acc[0..3], so only the tile's 64 output registers are live beside xb.
+  frag_t xb[UPF ? TP : 1][UPF ? 4 : 1];
+  auto stepT = [&](int g, int khalf) {   // one quadrant x K blocks 2 khalf, 2 khalf + 1: slot row 64 kbl + r
+    if constexpr (UPF) {
+      const char* Ws = wrow + (g % NS) * SLOT;
+      frag_t ar[3];
+      ar[0] = *reinterpret_cast<const frag_t*>(Ws);
+      ar[1] = *reinterpret_cast<const frag_t*>(Ws + 16 * 64);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int t = 0; t < TC; ++t) {   // t = 4 kbl + row group
+        if (t + 2 < TC) ar[(t + 2) % 3] = *reinterpret_cast<const frag_t*>(Ws + (t + 2) * 16 * 64);
+        const frag_t af = ar[t % 3];
+#pragma unroll
+        for (int p = 0; p < TP; ++p)
+          mfma_frag<T>(acc[t & 3][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, xb[p][2 * khalf + (t >> 2)]));
+        if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+      }
+    }
+  };
+  auto conv_to_xb = [&]() {   // bias + ReLU + cast (what EPI_STORE would store), then acc = 0
+    if constexpr (UPF) {
+      typedef T t8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          float bv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bv[j] = bias_s[64 * h + 16 * q + 8 * half + j];
+#pragma unroll
+          for (int p = 0; p < TP; ++p) {
+            t8 v;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (T)relu_nan(acc[4 * h + 2 * half + (j >> 2)][p][j & 3] + bv[j]);
+            xb[p][2 * h + half] = __builtin_bit_cast(frag_t, v);
+          }
+        }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)   // acc[0..3]: the ConvTranspose accumulators (acc[4..7] stay dead)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
   static_assert(SPC >= NS - 1, "a halo issued after an epilogue is first needed after the barrier-only waits");
   int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
   int wskip = 0;                            // barrier-only waits left after the last epilogue
@@ -1024,6 +1089,42 @@ __device__ __forceinline__ void ring_body(const IgemmArgs& a) {
         c = 0;
         tile_end = true;
       }
+    }
+    if (UPF && tile_end) {
+      // the conv part of the tile is done: its outputs become the B operand of the tile's SU
+      // ConvTranspose ring steps, run right here (so xb lives only inside this block); after each
+      // quadrant pair (4 steps) the pair's outputs are scattered into the concat buffer
+      conv_to_xb();
+      int n, ty, tx;
+      tile_of(item, n, ty, tx);
+#pragma nounroll
+      for (int quad = 0; quad < 4; ++quad) {   // (a, b) quadrant of the ConvTranspose: 64 output rows
+#pragma unroll
+        for (int khalf = 0; khalf < 2; ++khalf) {   // unrolled: xb[p][kb] must index registers
+          ++g;
+          if (g + NS - 1 < total) issue_w();
+          stepT(g, khalf);
+          int young = total - 2 - g;
+          young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
+          if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }
+          else ring_wait<TPS * WI, HI, NS - 2>(young, false);   // the last halo issue is older than W(g+1)
+        }
+        // no vmcnt(0) drain before the stores (unlike a tile end): the next step's wait (vmcnt of the
+        // loads issued after them) retires them, so they drain under that step's MFMAs
+        conv_epilogue<TO, TO, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[0]), n, ty * 16,
+                                                 tx * 16, wp * TP, 64 * quad, a.bias2 + 64 * quad, nullptr, nullptr,
+                                                 a.out2, a.ldo2, a.Cout / 2);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int t = 4; t < TC; ++t)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ++item;
+      continue;
     }
     if (tile_end) {
       int n, ty, tx;
@@ -1809,7 +1910,7 @@ static hipError_t launch_ring(const IgemmArgs& a, hipStream_t s) {
     if (a.Cin != 2 * G::BKE || a.c0 < 1 || a.c0 > 3 || !a.x0 || !a.w0p || !a.b0) return hipErrorInvalidValue;
   }
   if (a.tiles_y != (a.H + TH - 1) / TH || a.tiles_x != (a.W + TW - 1) / TW) return hipErrorInvalidValue;
-  if ((TH != 16 || TW != 16) && (long long)a.H * a.W * a.ldi * (long long)sizeof(T) >= (1LL << 31))
+  if ((TH != 16 || TW != 16 || EPI == EPI_UPFUSE) && (long long)a.H * a.W * a.ldi * (long long)sizeof(T) >= (1LL << 31))
     return hipErrorInvalidValue;   // 32-bit halo offsets (ring_body OFF32)
   if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
@@ -1847,6 +1948,13 @@ static hipError_t launch_tring(const IgemmArgs& a, hipStream_t s) {
 template <typename T, typename TO, typename TQ, int EPI, int ABL = 0>
 static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
   constexpr bool same = std::is_same<T, TO>::value && std::is_same<TO, TQ>::value;
+  if constexpr (EPI == EPI_UPFUSE) {   // conv2.3 + up1: the 16-bit 128-row ring only (one row tile)
+    if constexpr (sizeof(T) == 2 && ABL == 0) {
+      if (cfg == CFG_RING_R128 && a.n_ct == 1 && a.Cout == 128 && a.out2 && a.bias2)
+        return launch_ring<T, 1, 4, 8, 3, EPI_UPFUSE, 1, 0, TO, TQ>(a, s);
+    }
+    return hipErrorInvalidValue;
+  } else {
   if (EPI == EPI_HEAD && cfg_rows(cfg) != 64) return hipErrorInvalidValue;   // the head needs all 64 channels
   if constexpr (ABL != 0) {   // ablation builds: the ring configurations only
     switch (cfg) {
@@ -1887,6 +1995,7 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
     default: break;
   }
   return hipErrorInvalidValue;
+  }
 }
 
 // ConvTranspose2d(k2, s2) layers (1-tap GEMM + pixel-shuffle scatter).  TO = output type.
@@ -1929,6 +2038,7 @@ static hipError_t launch_typed(int cfg, int taps, int epi, const IgemmArgs& a, h
       case EPI_STORE: return launch_3x3<T, TO, TQ, EPI_STORE>(cfg, a, s);
       case EPI_POOL: return launch_3x3<T, TO, TQ, EPI_POOL>(cfg, a, s);
       case EPI_HEAD: return launch_3x3<T, TO, TQ, EPI_HEAD>(cfg, a, s);
+      case EPI_UPFUSE: return launch_3x3<T, TO, TQ, EPI_UPFUSE>(cfg, a, s);
       default: return hipErrorInvalidValue;
     }
   }
