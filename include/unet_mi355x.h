@@ -131,17 +131,19 @@ int unet_forward_boxes(unet_handle* h, const void* x, int x_layout, int x_dtype,
 int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channels,
                     float* x, int oh, int ow, void* hip_stream);
 
-/* Number of kernel launches in one forward (first conv, 17 implicit-GEMM 3x3 convs with
+/* Number of launch slots in one forward (first conv, 17 implicit-GEMM 3x3 convs with
  * the fused pool / head epilogues, 4 ConvTranspose2d), in execution order:
  * down1.0 down1.3 down2.0 down2.3 down3.0 down3.3 down4.0 down4.3 bottleneck.0
  * bottleneck.3 up4 conv4.0 conv4.3 up3 conv3.0 conv3.3 up2 conv2.0 conv2.3 up1 conv1.0
- * conv1.3+out_conv. */
+ * conv1.3+out_conv.  On the 16-bit plans up1 runs inside the conv2.3 launch (its slot issues no
+ * kernel: empty label, ~0 ms); the environment variable UNET_MI355X_FUSE_UP1=0, read by
+ * unet_create, keeps it a launch of its own. */
 #define UNET_NUM_LAUNCHES 22
 int unet_num_launches(void);
 
 /* Kernel instantiation run by launch i of a forward (e.g.
- * "conv3x3_ring_kernel<__bf16, 1, 4, 8, 3, 0, 1, 0, __bf16, __bf16>"), spelled like the demangled symbol that
- * rocprofv3 reports; "" for a bad index. */
+ * "conv3x3_ring_kernel<__bf16, 1, 4, 8, 3, 0, 1, 0, __bf16, __bf16, 16, 16>"), spelled like the demangled
+ * symbol that rocprofv3 reports; "" for a bad index or a slot fused into the previous launch. */
 const char* unet_launch_label(const unet_handle* h, int i);
 
 /* unet_forward, plus HIP-event timing of every launch on the given stream (ms, in the
@@ -154,7 +156,8 @@ int unet_forward_timed(unet_handle* h, const void* x, int x_layout, int x_dtype,
 /* Copy an intermediate activation of the last forward (debug / per-layer parity):
  * name in {"c1","p1","c2","p2","c3","p3","c4","p4","bn","c7","u1","u2","u3","u4","c8a"}
  * (c_k: encoder skips, p_k: pooled maps, u_k: ConvTranspose outputs, c7: conv2 output,
- * c8a: conv1.net.0 output).
+ * c8a: conv1.net.0 output).  "c7" is UNET_ESTATE after a forward with up1 fused into conv2.3
+ * (conv2's output then never leaves the registers; UNET_MI355X_FUSE_UP1=0 keeps it).
  * dst: device buffer receiving fp32 NCHW [N][C][h][w]; *numel receives the element count
  * when dst is NULL. */
 int unet_debug_fetch(unet_handle* h, const char* name, float* dst, size_t* numel, void* hip_stream);
