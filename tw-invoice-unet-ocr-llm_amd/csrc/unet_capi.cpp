@@ -161,12 +161,16 @@ const int kUpLevel[4] = {4, 3, 2, 1};   // input level of up4..up1
 //   down1.0 fused into down1.3 (tune_r1_ring_fused_in.txt).
 //   fp32: the 128-byte LDS-halo kernel (tune_r1.txt).
 //   round 2: the 8-wave 16x32-tile weight-stationary ring on the two Cin = 64 layers at 512^2
-//   (conv1.3 + head -14 %, down1.3 with the fused first conv -4 %: profiles/tune_r2_ring8*.txt).
+//   (conv1.3 + head -14 %, down1.3 with the fused first conv -4 %: profiles/tune_r2_ring8*.txt);
+//   session 2: the 8-wave 16x32-tile ring with 3 pipelined taps per step on every 128-row layer
+//   (-4..-11 % per layer, profiles/tune_r2j_ring8_r128_t3.txt) except conv2.3, which carries the
+//   fused up1 on the 4-wave ring (EPI_UPFUSE).
 const int kRingCfg[17] = {
     CFG_RING8_FUSED_IN,                                 // down1.0 + down1.3 (+pool), fused
-    CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128,
-    CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128, CFG_RING_R128,
-    CFG_RING_R128, CFG_RING_R128,                       // down2.0 .. conv2.3
+    CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128,
+    CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128,
+    CFG_RING8_R128,                                     // down2.0 .. conv2.0
+    CFG_RING_R128,                                      // conv2.3 (+ up1 fused)
     CFG_RING_R64_T3, CFG_RING8_R64_WS};                 // conv1.0, conv1.3 (+head)
 const int kHaloCfg[17] = {
     CFG_HALO_R64_W8,                                    // down1.3 (+pool)

@@ -52,11 +52,11 @@ bool cfg_is_ring8(int cfg) {
 int cfg_tile_w(int cfg) { return (cfg_is_ring8(cfg) || cfg % 16 == CFG_RING_R64_W12) ? 32 : 16; }
 int cfg_tile_h(int cfg) { return cfg % 16 == CFG_RING_R64_W12 ? 12 : 16; }
 bool cfg_fused_in(int cfg) { return cfg % 16 == CFG_RING_FUSED_IN || cfg % 16 == CFG_RING8_FUSED_IN; }
-int ring_ns(int cfg) { return (cfg % 16 == CFG_RING8_R128 || cfg % 16 == CFG_RING_R64_W12) ? 4 : 3; }
+int ring_ns(int cfg) { return cfg % 16 == CFG_RING_R64_W12 ? 4 : 3; }
 int ring_tps(int cfg) {
   cfg %= 16;
-  return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS ||
-          cfg == CFG_RING8_FUSED_IN) ? 3 : 1;
+  return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_T3 ||
+          cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN) ? 3 : 1;
 }
 int cfg_limit() {
 #ifdef UNET_ABLATION
@@ -430,6 +430,39 @@ __device__ __forceinline__ void mfma_taps(f32x4 (&acc)[TC][TP], const char* cons
       }
     } else {
       __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+    }
+  }
+}
+
+// The same for wide row tiles (TC = 8: 8 A + 4 B fragments per tap would need 96 registers
+// double-buffered): the A fragments of all NT taps form ONE stream through a 3-register ring two
+// row groups ahead (crossing tap boundaries), and only the TP B fragments are double-buffered --
+// tap k+1's are read under the first TP row groups of tap k.
+template <typename T, int TC, int TP, int NT>
+__device__ __forceinline__ void mfma_taps_astream(f32x4 (&acc)[TC][TP], const char* const (&hs)[NT],
+                                                  const char* const (&ws)[NT], const int (&prow)[TP]) {
+  static_assert(TC >= TP && TC >= 3, "B prefetch spread over the row groups");
+  frag_t ar[3], fb[2][TP];
+  auto lda = [&](int j) { return *reinterpret_cast<const frag_t*>(ws[j / TC] + (j % TC) * 16 * 64); };
+#pragma unroll
+  for (int p = 0; p < TP; ++p) fb[0][p] = *reinterpret_cast<const frag_t*>(hs[0] + prow[p]);
+  ar[0] = lda(0);
+  ar[1] = lda(1);
+  __builtin_amdgcn_sched_group_barrier(0x100, TP + 2, 0);
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+#pragma unroll
+    for (int t = 0; t < TC; ++t) {
+      const int j = k * TC + t;
+      if (j + 2 < NT * TC) ar[(j + 2) % 3] = lda(j + 2);
+      if (k + 1 < NT && t < TP) fb[(k + 1) & 1][t] = *reinterpret_cast<const frag_t*>(hs[k + 1] + prow[t]);
+      const frag_t af = ar[j % 3];
+#pragma unroll
+      for (int p = 0; p < TP; ++p)
+        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, fb[k & 1][p]));
+      if (j + 2 < NT * TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if (k + 1 < NT && t < TP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
     }
   }
 }
@@ -1552,7 +1585,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         }
         mfma_taps<T, TC, TP, 9>(acc, hs9, ws9, prow);
       }
-    } else if constexpr (TPS == 3 && TC * TP % (TC + TP) == 0) {
+    } else if constexpr (TPS == 3) {
       const int wslot = WST ? g - (g / S) * S : g % NS;
       const char* hs3[3];
       const char* ws3[3];
@@ -1561,7 +1594,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         hs3[t] = lds + (hseq & 1) * HALO_BYTES + (tap * HWD + t) * 64 + ((q ^ ((px_lane + t) & 3)) << 4);
         ws3[t] = wrow + wslot * SLOT + t * WSLOT;
       }
-      mfma_taps<T, TC, TP, 3>(acc, hs3, ws3, prow);
+      if constexpr (TC * TP % (TC + TP) == 0) mfma_taps<T, TC, TP, 3>(acc, hs3, ws3, prow);
+      else mfma_taps_astream<T, TC, TP, 3>(acc, hs3, ws3, prow);
     } else {
 #pragma unroll
       for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
@@ -1986,7 +2020,7 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
     case CFG_RING_FUSED_IN:
       if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
       break;
-    case CFG_RING8_R128: if constexpr (EPI != EPI_HEAD) return launch_ring8<T, 8, 4, EPI, 1, 0, TO, TQ>(a, s); break;
+    case CFG_RING8_R128: if constexpr (EPI != EPI_HEAD) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ>(a, s); break;
     case CFG_RING8_R64_T3: return launch_ring8<T, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
     case CFG_RING8_R64_WS: return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
     case CFG_RING8_FUSED_IN:
