@@ -163,14 +163,13 @@ const int kUpLevel[4] = {4, 3, 2, 1};   // input level of up4..up1
 //   round 2: the 8-wave 16x32-tile weight-stationary ring on the two Cin = 64 layers at 512^2
 //   (conv1.3 + head -14 %, down1.3 with the fused first conv -4 %: profiles/tune_r2_ring8*.txt);
 //   session 2: the 8-wave 16x32-tile ring with 3 pipelined taps per step on every 128-row layer
-//   (-4..-11 % per layer, profiles/tune_r2j_ring8_r128_t3.txt) except conv2.3, which carries the
-//   fused up1 on the 4-wave ring (EPI_UPFUSE).
+//   (-4..-11 % per layer, profiles/tune_r2j_ring8_r128_t3.txt), conv2.3 with the fused up1
+//   (EPI_UPFUSE) included (-5.5 %, tune_r2j_fused_up1.txt).
 const int kRingCfg[17] = {
     CFG_RING8_FUSED_IN,                                 // down1.0 + down1.3 (+pool), fused
     CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128,
     CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128,
-    CFG_RING8_R128,                                     // down2.0 .. conv2.0
-    CFG_RING_R128,                                      // conv2.3 (+ up1 fused)
+    CFG_RING8_R128, CFG_RING8_R128,                     // down2.0 .. conv2.3 (+ up1 fused)
     CFG_RING_R64_T3, CFG_RING8_R64_WS};                 // conv1.0, conv1.3 (+head)
 const int kHaloCfg[17] = {
     CFG_HALO_R64_W8,                                    // down1.3 (+pool)
@@ -318,10 +317,13 @@ int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::v
 // slot row 64 kbl + rr = packed row rho = 64 * quadrant + rr (natural row natural_of_packed(rho) =
 // quadrant x 64 + o) of K block kb, K slot 8q + j <-> input channel 64 * (kb >> 1) + 16q + 8 * (kb & 1)
 // + j (the channels each lane of the conv's accumulators holds, ring_body EPI_UPFUSE).
+// The 8-wave ring (CFG_RING8_R128, 24 KB slots of 3 taps) takes the same conv bytes and 4
+// ConvTranspose slots instead, one quadrant each: slot row 64 kb + rr (kb = 0..3), rows 256..383 zero.
 int pack_fused_up(unet_handle* h, const Layer& L, const Layer& U, const std::vector<double>& w, const float* Wt) {
   const int BR = 128, BKE = 64 / (int)dtype_size(L.dt), S = 9 * L.cin / BKE;
+  const bool ring8 = L.cfg == CFG_RING8_R128;
   if (L.cout != BR || U.cin != BR || U.cout != 64 || BKE != 32) return fail(UNET_EINVAL, "fused up1: layer shapes");
-  std::vector<uint8_t> buf((size_t)(S + 8) * BR * BKE * dtype_size(L.dt));
+  std::vector<uint8_t> buf((size_t)(S + 8 + (ring8 ? 4 : 0)) * BR * BKE * dtype_size(L.dt));
   for (int rho = 0; rho < BR; ++rho) {
     const int o = natural_of_packed(rho);
     for (int tap = 0; tap < 9; ++tap)
@@ -329,14 +331,16 @@ int pack_fused_up(unet_handle* h, const Layer& L, const Layer& U, const std::vec
         put_elem(L.dt, buf, ((size_t)((c / BKE) * 9 + tap) * BR + rho) * BKE + c % BKE, w[((size_t)o * L.cin + c) * 9 + tap]);
   }
   for (int u = 0; u < 8; ++u) {
+    // 4-wave ring: step u = (quadrant u >> 1, K blocks 2 (u & 1) + kbl), slot row 64 kbl + rr;
+    // 8-wave ring: 128-row block u of the 4 x 384-row quadrant slots (rows 64 kb + rr, zero past 256)
     const int quad = u >> 1, khalf = u & 1;
-    for (int r = 0; r < BR; ++r) {   // slot row r = 64 kbl + rr: quadrant row rr, K block 2 khalf + kbl
+    for (int r = 0; r < BR; ++r) {
       const int kb = 2 * khalf + (r >> 6);
       const int nat = natural_of_packed(64 * quad + (r & 63)), ab = nat / 64, o = nat % 64;
+      const size_t row = ring8 ? (size_t)S * BR + (size_t)quad * 3 * BR + 64 * kb + (r & 63) : (size_t)(S + u) * BR + r;
       for (int sl = 0; sl < 32; ++sl) {
         const int c = 64 * (kb >> 1) + 16 * (sl >> 3) + 8 * (kb & 1) + (sl & 7);
-        put_elem(L.dt, buf, ((size_t)(S + u) * BR + r) * BKE + sl,
-                 Wt[(((size_t)c * U.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]);
+        put_elem(L.dt, buf, row * BKE + sl, Wt[(((size_t)c * U.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]);
       }
     }
   }
@@ -668,7 +672,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   {
     const char* fz = std::getenv("UNET_MI355X_FUSE_UP1");
     const Layer &c2b = h->L[C2B], &u1 = h->U[3];
-    h->fuse_up1 = !(fz && fz[0] == '0') && !f32 && c2b.cfg == CFG_RING_R128 && u1.dt == c2b.dt && u1.dto == c2b.dto;
+    h->fuse_up1 = !(fz && fz[0] == '0') && !f32 && (c2b.cfg == CFG_RING_R128 || c2b.cfg == CFG_RING8_R128) &&
+                  u1.dt == c2b.dt && u1.dto == c2b.dto;
   }
   build_labels(h);   // after every layer's configuration (3x3 and ConvTranspose) is final
   DeviceGuard g(cfg->device);

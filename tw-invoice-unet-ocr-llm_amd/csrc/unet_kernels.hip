@@ -1279,6 +1279,12 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   static_assert(G::LDS_BYTES <= 160 * 1024, "LDS");
   static_assert(HS == 0 || (WST && sizeof(T) == 2 && BR == 64 && TPS == 3 && EPI != EPI_HEAD),
                 "fused first conv: weight-stationary 16-bit 64-row ring, 3 taps per step");
+  // EPI_UPFUSE (conv2.3 + up1, see ring_body): after a tile's conv steps, SU = 4 more ring steps,
+  // one (a, b) quadrant each: 64 rows x 128 K of ConvTranspose weights (16 KB of the 24 KB slot,
+  // pseudo-row 64 kb + r), 64 MFMAs per wave; B = the tile's conv outputs in registers.
+  constexpr bool UPF = EPI == EPI_UPFUSE;
+  static_assert(!UPF || (sizeof(T) == 2 && TC == 8 && TPS == 3 && WST == 0 && HS == 0), "fused ConvTranspose");
+  constexpr int SU = UPF ? 4 : 0;
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
   float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
   float* headw_s = bias_s + BR;
@@ -1304,15 +1310,16 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 
   const int H = a.H, W = a.W;
   const int nch = a.Cin / BKE;
-  const int S = SPC * nch;
-  const int total = items * S;
+  const int S = SPC * nch;       // conv steps per tile
+  const int ST = S + SU;         // ring steps per tile
+  const int total = items * ST;
   const int hseq_end = items * nch;
   // weight DMA pieces of this wave per step: pieces wave, wave + 8, ... of the step's PIECES
   const int wcnt = (PIECES - wave + NW - 1) / NW;
 
   // weights of row tile ct in step order (the 4-wave ring's packing): piece j of a step = rows
   // 16j .. 16j+15; per lane one 16-byte chunk of row 16j + lane/4 at position chunk ^ ((row>>1)&3)
-  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * SLOT + (lane >> 2) * 64 +
+  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * ST * SLOT + (lane >> 2) * 64 +
                      (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
   const char* in = reinterpret_cast<const char*>(a.in);
   const char* zero = reinterpret_cast<const char*>(a.zero);
@@ -1362,7 +1369,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   int wq_s = 0, wq_slot = 0;
   auto issue_w = [&]() {
     issue_w_step(wq_s, wq_slot);
-    if (++wq_s == S) wq_s = 0;
+    if (++wq_s == ST) wq_s = 0;
     if (++wq_slot == NS) wq_slot = 0;
   };
 
@@ -1563,6 +1570,50 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     }
     return;
   }
+  frag_t xb[UPF ? TP : 1][UPF ? 4 : 1];   // EPI_UPFUSE: see ring_body
+  auto conv_to_xb = [&]() {
+    if constexpr (UPF) {
+      typedef T t8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          float bv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bv[j] = bias_s[64 * h + 16 * q + 8 * half + j];
+#pragma unroll
+          for (int p = 0; p < TP; ++p) {
+            t8 v;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (T)relu_nan(acc[4 * h + 2 * half + (j >> 2)][p][j & 3] + bv[j]);
+            xb[p][2 * h + half] = __builtin_bit_cast(frag_t, v);
+          }
+        }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto stepT = [&](int g) {   // one quadrant: acc[t] += A(kb, t) x xb[kb], kb = 0..3 (the ring's K order)
+    if constexpr (UPF) {
+      const char* Ws = wrow + (g % NS) * SLOT;
+      frag_t ar[3];
+      ar[0] = *reinterpret_cast<const frag_t*>(Ws);
+      ar[1] = *reinterpret_cast<const frag_t*>(Ws + 16 * 64);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {   // j = 4 kb + t
+        if (j + 2 < 16) ar[(j + 2) % 3] = *reinterpret_cast<const frag_t*>(Ws + (j + 2) * 16 * 64);
+        const frag_t af = ar[j % 3];
+#pragma unroll
+        for (int p = 0; p < TP; ++p)
+          mfma_frag<T>(acc[j & 3][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, xb[p][j >> 2]));
+        if (j + 2 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+      }
+    }
+  };
   static_assert(WST || SPC >= NS - 1, "see ring_body");
   int wskip = 0;
   int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
@@ -1623,6 +1674,35 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         c = 0;
         tile_end = true;
       }
+    }
+    if (UPF && tile_end) {   // the tile's SU ConvTranspose steps, right here (see ring_body)
+      conv_to_xb();
+      int n, ty, tx;
+      tile_of(item, n, ty, tx);
+#pragma nounroll
+      for (int quad = 0; quad < SU; ++quad) {
+        ++g;
+        if (g + NS - 1 < total) issue_w();
+        stepT(g);
+        int young = total - 2 - g;
+        young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
+        if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }
+        else wait_vm_barrier_rt(young * wcnt);   // the last halo issue is older than W(g+1)
+        // no vmcnt(0) drain: the stores retire under the next step's wait (see ring_body)
+        conv_epilogue<TO, TO, TP, EPI_UPSCATTER, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[0]), n, ty * 16,
+                                                     tx * TW, wp * TP, 64 * quad, a.bias2 + 64 * quad, nullptr,
+                                                     nullptr, a.out2, a.ldo2, a.Cout / 2);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int t = 4; t < TC; ++t)
+#pragma unroll
+        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ++item;
+      continue;
     }
     if (tile_end) {
       int n, ty, tx;
@@ -1986,6 +2066,8 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
     if constexpr (sizeof(T) == 2 && ABL == 0) {
       if (cfg == CFG_RING_R128 && a.n_ct == 1 && a.Cout == 128 && a.out2 && a.bias2)
         return launch_ring<T, 1, 4, 8, 3, EPI_UPFUSE, 1, 0, TO, TQ>(a, s);
+      if (cfg == CFG_RING8_R128 && a.n_ct == 1 && a.Cout == 128 && a.out2 && a.bias2)
+        return launch_ring8<T, 8, 3, EPI_UPFUSE, 3, 0, TO, TQ>(a, s);
     }
     return hipErrorInvalidValue;
   } else {
