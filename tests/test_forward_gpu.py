@@ -529,7 +529,11 @@ def test_fused_up1_matches_unfused(dtype, monkeypatch):
             monkeypatch.setenv("UNET_MI355X_FUSE_UP1", fuse)
             m = make_model(sd, 3, dtype)
             st[fuse] = _forward_state(m, x)
+            labels = m.native_handle(torch.device(DEV)).launch_labels()
+            assert (labels[19] == "") == (fuse == "1"), labels[19]   # up1's slot: fused -> no launch
             if fuse == "1":
+                epi_arg = 3 if labels[18].startswith("conv3x3_ring8_kernel") else 5
+                assert labels[18].split(",")[epi_arg].strip() == "4", labels[18]   # conv2.3: EPI_UPFUSE
                 assert "c7" not in st[fuse]
                 assert _first_diff(_forward_state(m, x), st[fuse]) == []
             m.close()
