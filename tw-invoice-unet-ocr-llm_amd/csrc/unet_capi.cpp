@@ -164,13 +164,14 @@ const int kUpLevel[4] = {4, 3, 2, 1};   // input level of up4..up1
 //   (conv1.3 + head -14 %, down1.3 with the fused first conv -4 %: profiles/tune_r2_ring8*.txt);
 //   session 2: the 8-wave 16x32-tile ring with 3 pipelined taps per step on every 128-row layer
 //   (-4..-11 % per layer, profiles/tune_r2j_ring8_r128_t3.txt), conv2.3 with the fused up1
-//   (EPI_UPFUSE) included (-5.5 %, tune_r2j_fused_up1.txt).
+//   (EPI_UPFUSE) included (-5.5 %, tune_r2j_fused_up1.txt); conv1.0 on the 8-wave 64-row ring with
+//   a whole 32-channel chunk (9 pipelined taps) per step (-11 %, tune_r2j_ring8_r64_t9.txt).
 const int kRingCfg[17] = {
     CFG_RING8_FUSED_IN,                                 // down1.0 + down1.3 (+pool), fused
     CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128,
     CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128, CFG_RING8_R128,
     CFG_RING8_R128, CFG_RING8_R128,                     // down2.0 .. conv2.3 (+ up1 fused)
-    CFG_RING_R64_T3, CFG_RING8_R64_WS};                 // conv1.0, conv1.3 (+head)
+    CFG_RING8_R64_T9, CFG_RING8_R64_WS};                // conv1.0 (one chunk per step), conv1.3 (+head)
 const int kHaloCfg[17] = {
     CFG_HALO_R64_W8,                                    // down1.3 (+pool)
     CFG_HALO_R128, CFG_HALO_R128, CFG_HALO_R128, CFG_HALO_R64_W4, CFG_HALO_R128, CFG_HALO_R64_W4,
@@ -649,8 +650,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     // configurations of a family accumulate in the same K order, so they agree bitwise)
     const bool ring = cfg_is_ring(c);
     if (cfg_fused_in(c) && (i != D1B || f32)) c = L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128;
-    if (c == CFG_RING8_R64_WS && (L.cin != 64 || f32)) c = L.cout == 64 ? CFG_RING8_R64_T3 : CFG_RING8_R128;   // 72 KB of weights max
-    if (c == CFG_RING8_R128 && L.cout == 64) c = CFG_RING8_R64_T3;
+    if (c == CFG_RING8_R64_WS && (L.cin != 64 || f32)) c = L.cout == 64 ? CFG_RING8_R64_T9 : CFG_RING8_R128;   // 72 KB of weights max
+    if (c == CFG_RING8_R128 && L.cout == 64) c = CFG_RING8_R64_T9;
     if (c == CFG_RING_R64_W12 && f32) c = CFG_RING_R64_T3;   // 16-bit only
     if (cfg_rows(c) > L.cout || (i == C1B && cfg_rows(c) != 64))
       c = ring ? CFG_RING_R64_T3 : CFG_HALO_R64_W8;

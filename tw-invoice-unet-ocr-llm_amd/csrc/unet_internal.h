@@ -92,7 +92,7 @@ enum Cfg : int {
   CFG_TRING_R256 = 7,     // ConvTranspose ring: 8 waves, 256-row x 256-pixel block tiles, 4 slots
   // 8-wave ring over 16x32 pixel tiles, one block per CU (half the weight bytes per MFMA)
   CFG_RING8_R128 = 8,     // 128 rows, 3 taps per step (pipelined A-fragment stream), 3 slots
-  CFG_RING8_R64_T3 = 9,   // 64 rows, 3 taps per step, 3 slots
+  CFG_RING8_R64_T9 = 9,   // 64 rows, one 32-channel chunk (9 pipelined taps) per step, 2 slots of 36 KB
   CFG_RING8_R64_WS = 10,  // 64 rows, 3 taps per step, weight-stationary (Cin = 64)
   CFG_RING8_FUSED_IN = 11,// RING8_R64_WS for down1.3 with down1.0 fused
   // 4-wave ring over 12x32 pixel tiles, two blocks per CU: 384 pixels per weight step (1.5x the

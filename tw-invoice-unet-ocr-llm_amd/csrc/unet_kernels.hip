@@ -43,20 +43,21 @@ bool cfg_is_halo(int cfg) { return cfg == CFG_HALO_R64_W4 || cfg == CFG_HALO_R64
 bool cfg_is_ring(int cfg) {
   cfg %= 16;
   return cfg == CFG_RING_R128 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R128 ||
-         cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN || cfg == CFG_RING_R64_W12;
+         cfg == CFG_RING8_R64_T9 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN || cfg == CFG_RING_R64_W12;
 }
 bool cfg_is_ring8(int cfg) {
   cfg %= 16;
-  return cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_T3 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;
+  return cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_T9 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;
 }
 int cfg_tile_w(int cfg) { return (cfg_is_ring8(cfg) || cfg % 16 == CFG_RING_R64_W12) ? 32 : 16; }
 int cfg_tile_h(int cfg) { return cfg % 16 == CFG_RING_R64_W12 ? 12 : 16; }
 bool cfg_fused_in(int cfg) { return cfg % 16 == CFG_RING_FUSED_IN || cfg % 16 == CFG_RING8_FUSED_IN; }
-int ring_ns(int cfg) { return cfg % 16 == CFG_RING_R64_W12 ? 4 : 3; }
+int ring_ns(int cfg) { return cfg % 16 == CFG_RING_R64_W12 ? 4 : (cfg % 16 == CFG_RING8_R64_T9 ? 2 : 3); }
 int ring_tps(int cfg) {
   cfg %= 16;
-  return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_T3 ||
-          cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN) ? 3 : 1;
+  if (cfg == CFG_RING8_R64_T9) return 9;
+  return (cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_WS ||
+          cfg == CFG_RING8_FUSED_IN) ? 3 : 1;
 }
 int cfg_limit() {
 #ifdef UNET_ABLATION
@@ -1273,8 +1274,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   constexpr int HWD = G::HWD, HP = G::HP, HI = G::HI, HALO_BYTES = G::HALO_BYTES;
   constexpr int WSLOT = G::WSLOT, SLOT = G::SLOT, PIECES = G::PIECES, WOFF = G::WOFF;
   constexpr int SPC = 9 / TPS;   // steps per 32-channel chunk
-  static_assert(TPS == 1 || TPS == 3, "taps per step");
-  static_assert(WST || (NS >= 3 && NS <= 4), "weight ring depth");
+  static_assert(TPS == 1 || TPS == 3 || (TPS == 9 && !WST && HS == 0), "taps per step");
+  static_assert(WST || (NS >= 3 && NS <= 4) || (TPS == 9 && NS == 2), "weight ring depth");
   static_assert(EPI != EPI_HEAD || BR == 64, "fused head needs the 64 channels in one block");
   static_assert(G::LDS_BYTES <= 160 * 1024, "LDS");
   static_assert(HS == 0 || (WST && sizeof(T) == 2 && BR == 64 && TPS == 3 && EPI != EPI_HEAD),
@@ -1636,6 +1637,18 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         }
         mfma_taps<T, TC, TP, 9>(acc, hs9, ws9, prow);
       }
+    } else if constexpr (TPS == 9) {
+      // one step = a whole 32-channel chunk (nine taps, one barrier): the weights of the next chunk
+      // (36 KB) and its halo load during this one (2-slot ring), and all nine taps are pipelined
+      const char* hs9[9];
+      const char* ws9[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {   // tap (dy, dx) = (k / 3, k % 3)
+        const int dy = k / 3, dx = k % 3;
+        hs9[k] = lds + (hseq & 1) * HALO_BYTES + (dy * HWD + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
+        ws9[k] = wrow + (g % NS) * SLOT + k * WSLOT;
+      }
+      mfma_taps<T, TC, TP, 9>(acc, hs9, ws9, prow);
     } else if constexpr (TPS == 3) {
       const int wslot = WST ? g - (g / S) * S : g % NS;
       const char* hs3[3];
@@ -2103,7 +2116,7 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
       if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
       break;
     case CFG_RING8_R128: if constexpr (EPI != EPI_HEAD) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ>(a, s); break;
-    case CFG_RING8_R64_T3: return launch_ring8<T, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
+    case CFG_RING8_R64_T9: return launch_ring8<T, 4, 2, EPI, 9, 0, TO, TQ>(a, s);
     case CFG_RING8_R64_WS: return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
     case CFG_RING8_FUSED_IN:
       if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ, 1>(a, s);
