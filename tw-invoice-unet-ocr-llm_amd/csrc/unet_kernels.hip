@@ -1720,10 +1720,10 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     if (tile_end) {
       int n, ty, tx;
       tile_of(item, n, ty, tx);
-      if (!WST) {   // see ring_body: the next NS-2 waits are barriers only
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        wskip = NS - 2;
-      }
+      // No vmcnt(0) drain before the stores (the 4-wave ring's habit): with one block per CU that
+      // drain (the next steps' weights and halo, issued up to NS-1 steps ahead) is exposed once per
+      // tile.  The stores are issued after those loads, so the next step's counted wait (for loads
+      // issued after them) retires them under that step's MFMAs.
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
         conv_epilogue<TO, TQ, TP, EPI, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
