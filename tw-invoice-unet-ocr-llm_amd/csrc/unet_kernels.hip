@@ -1884,8 +1884,12 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
       c = 0;
       int n, ty, tx;
       tile_of(item, n, ty, tx);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // steps g+2 .. g+NS-1 landed before the stores
-      wskip = NS - 2;
+      // no vmcnt(0) drain before the stores with one block per CU (exposed): the next steps' counted
+      // waits retire them (see conv3x3_ring8_kernel); the two-block configuration keeps the drain
+      if (WRW == 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // steps g+2 .. g+NS-1 landed before the stores
+        wskip = NS - 2;
+      }
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
         conv_epilogue<TO, TO, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
