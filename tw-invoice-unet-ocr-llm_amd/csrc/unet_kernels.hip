@@ -1620,8 +1620,11 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   int c = 0, tap = 0, hseq = 0, item = 0;   // tap = step index within the chunk (0 .. SPC-1)
   for (int g = 0; g < total; ++g) {
     const bool hnext = tap == 0 && hseq + 1 < hseq_end;
-    if (HS == 0 && hnext) issue_halo();
+    // the next chunk's halo is issued AFTER this step's weights: vmcnt retires in issue order, so
+    // the halo then stays in flight through the wait for W(g+2) too (NS - 1 steps of latency
+    // instead of NS - 2; it is needed only at the chunk end)
     if (!WST && g + NS - 1 < total) issue_w();
+    if (HS == 0 && hnext) issue_halo();
     if constexpr (WST && HS == 0 && TPS == 3 && TC * TP % (TC + TP) == 0) {
       // weight-stationary, DMA'd halo: no barrier inside a chunk, so its nine taps (three steps)
       // run as one pipelined sequence at the chunk's first step; the other two only keep count
@@ -1672,10 +1675,10 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     } else {
       // W(g+1) must have landed (and, at a chunk end, the next halo -- issued SPC-1 steps
       // earlier, older than W(g+1)).  Younger loads may stay in flight: W(g+2 .. g+NS-1) and a
-      // halo issued within the last NS-2 steps.
+      // halo issued within the last NS-1 steps (after W(g+1) -- issued NS-2 steps ago).
       int young = total - 2 - g;
       young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
-      const bool hyoung = tap < NS - 2 && hseq + 1 < hseq_end;
+      const bool hyoung = tap < NS - 1 && tap < SPC - 1 && hseq + 1 < hseq_end;
       if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }   // see ring_body
       else wait_vm_barrier_rt(young * wcnt + (hyoung ? HI : 0));
     }
