@@ -4,16 +4,26 @@
 One step = one pass of the hot path over one batch of synthetic invoice pages resident in
 HBM: UNet(3,3) forward at 512x512 (unet_model.py:55-86) with the fused sigmoid +
 per-field threshold (inference.py:72-79) producing bit-packed masks, plus -- for N>1 --
-the RCCL all-gather of the masks over xGMI.  Per-GPU batch is fixed (weak scaling).
+the RCCL all-gather of the masks over xGMI into a preallocated buffer.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--dtype mixed]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--global-batch G] [--dtype mixed]
     torchrun --nproc-per-node N bench.py --gpus N ...      (the driver does this for N>1)
 
-Rank 0 prints ONE JSON line.  Extra fields: roofline (dominant kernel, HIP-event timed
-inside this run), cpu_baseline (the oracle on this host's cores, bounded sample: batch-1 and
-batch-8 forward, run_unet end to end with its model load, and the mask IoU of the GPU masks
-against the CPU masks), latency_bs1 (the drop-in run_unet and the batch-1 forward, eager and
-hipGraph), kernels (per-instantiation time breakdown).
+Launch: under torchrun (WORLD_SIZE set) every process is one rank; WORLD_SIZE must equal --gpus
+(exit 2 otherwise).  Without WORLD_SIZE and --gpus N > 1 the script spawns its own N rank
+processes (127.0.0.1 rendezvous) before any GPU call and exits with the worst rank's code.
+
+Scaling: by default every GPU holds --batch images per step (weak scaling, the headline `value`);
+--global-batch G splits G images over the ranks instead (strong scaling).  The same run also
+times the strong-scaling shapes of BASELINE's multi-GPU configurations -- global batch 256
+(north_star's "1 -> 8 GPUs at batch 256": 32 images per rank at N = 8) and 1024 (config 4: 128
+per rank) -- as `strong_scaling`.
+
+Rank 0 prints ONE JSON line.  Extra fields: roofline (dominant kernel, HIP-event timed inside
+this run), cpu_baseline (the oracle on this host's cores, bounded sample), fp32 (BASELINE
+config 2: batch 32, 512^2, the drop-in's default precision, against the 157.3 TF fp32 MFMA
+peak), latency_bs1 (the drop-in run_unet and the batch-1 forward at the drop-in default fp32
+and at the bench plan), kernels (per-instantiation time breakdown).
 """
 from __future__ import annotations
 
@@ -21,6 +31,8 @@ import argparse
 import json
 import os
 import re
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -33,17 +45,17 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from unet_mi355x import native  # noqa: E402
 from unet_mi355x import dist as udist  # noqa: E402
 from unet_mi355x import synthetic as syn  # noqa: E402
-from unet_mi355x.model import UNet  # noqa: E402
 
 METRIC = "invoice masks/sec at 512x512 bs256, 1/2/4/8 MI355X; IoU vs CPU ref"
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "mixed": 2500.0, "fp32": 157.3}   # dense MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
 PLAN = {"mixed": "bf16 storage at resolution levels 2-4 (64..1024 ch, 128^2..32^2), fp16 at levels 0-1 "
                  "(512^2, 256^2); fp32 accumulation, fp32 head",
         "bf16": "bf16 storage, fp32 accumulation, fp32 head", "fp16": "fp16 storage, fp32 accumulation, fp32 head",
         "fp32": "fp32 (exact-fp32 MFMA)"}
+STRONG_GLOBAL = (256, 1024)   # north_star's batch 256 and BASELINE config 4's batch 1024
 
 # launch order of include/unet_mi355x.h: (name, cin, cout, input level, kind); the kernel
 # instantiation of each launch comes from the library (unet_launch_label)
@@ -93,7 +105,7 @@ def mangled(label):
 
 
 def launch_flops(entry, n, h, w, c_in, ncls=3):
-    """Algorithmic FLOPs (2 per MAC) of one launch over n images of h x w."""
+    """Algorithmic FLOPs (2 per MAC) of one layer over n images of h x w."""
     name, cin, cout, lvl, kind = entry
     hh, ww = h >> lvl, w >> lvl
     if kind == "first":
@@ -107,8 +119,8 @@ def launch_flops(entry, n, h, w, c_in, ncls=3):
 
 
 def launch_bytes(entry, n, h, w, c_in, esize, ncls=3):
-    """Algorithmic HBM bytes of one launch: every activation read once and written once,
-    weights read once, concat zero-copy, BN/ReLU/pool/head fused."""
+    """Algorithmic HBM bytes of one layer as its own launch: every activation read once and
+    written once, weights read once, concat zero-copy, BN/ReLU/pool/head fused."""
     name, cin, cout, lvl, kind = entry
     hh, ww = h >> lvl, w >> lvl
     if kind == "first":
@@ -124,9 +136,39 @@ def launch_bytes(entry, n, h, w, c_in, esize, ncls=3):
     return b
 
 
+def launch_table(labels, n, h, w, c_in, esize, ncls=3):
+    """Per launch slot: (layer name, kernel label, FLOPs, algorithmic bytes, issues a dispatch).
+
+    Fusions move work between slots so that no slot is credited with work its kernel does not do:
+      * slot 0 = x_to_px4 (16-bit plans): the input pre-cast only (fp32 NCHW read, C -> 4
+        channels at esize written); down1.0's FLOPs and weights go to the fused down1.3, which
+        reads the 4-channel input instead of a 64-channel map;
+      * an empty label (up1 inside conv2.3): the ConvTranspose's FLOPs and its weight + output
+        bytes go to the previous launch, whose own output (up1's input) never reaches HBM."""
+    rows = []
+    for entry, lab in zip(LAUNCHES, labels):
+        f = launch_flops(entry, n, h, w, c_in, ncls)
+        b = launch_bytes(entry, n, h, w, c_in, esize, ncls)
+        rows.append([entry[0], lab, f, b, bool(lab)])
+    if labels[0].startswith("x_to_px4"):
+        rows[1][2] += rows[0][2]
+        rows[1][3] += 9 * c_in * 64 * esize - n * h * w * 64 * esize + n * h * w * 4 * esize
+        rows[0][2] = 0.0
+        rows[0][3] = n * c_in * h * w * 4 + n * h * w * 4 * esize
+    for i, r in enumerate(rows):
+        if not r[4] and i > 0:    # fused into the previous launch
+            _, cin, _, lvl, _ = LAUNCHES[i]
+            prev = rows[i - 1]
+            prev[2] += r[2]
+            # its input (the previous launch's output) is neither written nor read again
+            prev[3] += r[3] - 2 * n * (h >> lvl) * (w >> lvl) * cin * esize
+            r[1], r[2], r[3] = prev[1], 0.0, 0
+    return [tuple(r) for r in rows]
+
+
 def gen_pages(seed, batch, size, channels, unique=32):
     """Synthetic invoice pages; `unique` distinct pages tiled to the batch (generation cost)."""
-    u = min(unique, batch)
+    u = max(1, min(unique, batch))
     pages = syn.invoice_pages(seed, u, size, size, channels)
     reps = (batch + u - 1) // u
     return np.ascontiguousarray(np.concatenate([pages] * reps, axis=0)[:batch])
@@ -156,7 +198,222 @@ def host_cores():
     return use, {"os_cpu_count": total, "affinity": avail, "cgroup_quota": quota, "cpu_model": model}
 
 
-def cpu_baseline(args, model, x, masks, C, S):
+# ----------------------------------------------------------------------------- launching
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n, argv, timeout=None):
+    """Run this script as n rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, the
+    torchrun contract) and return the worst exit code.  The caller has made no GPU call (a process
+    that initialised the GPU must not hand over to others, and the ranks pick their own device).
+    If one rank fails the others are stopped (their exact PIDs), so a lost peer cannot hang the job."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    t0, rcs, first_bad = time.time(), [None] * n, None
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+                if rcs[i] not in (None, 0) and first_bad is None:
+                    first_bad = rcs[i]     # the root cause, not the peers stopped below
+        if first_bad is not None or (timeout and time.time() - t0 > timeout):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                try:
+                    rcs[i] = p.wait(timeout=30) if rcs[i] is None else rcs[i]
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    if first_bad is not None:
+        return first_bad if first_bad > 0 else 128 - first_bad    # a signal -> 128 + signum
+    return 0 if all(rc == 0 for rc in rcs) else 124                # timed out
+
+
+# ----------------------------------------------------------------------------- per-rank runners
+class NativeRunner:
+    """The product path: UNet on the native library, forward of a shard into bit-packed masks."""
+
+    def __init__(self, args, dev, world):
+        from unet_mi355x import native
+        from unet_mi355x.model import UNet
+        self.native, self.dev, self.args = native, dev, args
+        C = args.channels
+        # weights: the real checkpoint is an LFS pointer, so the seeded synthetic weights with the
+        # fine-tuned BN/bias subset ("pretrained", tools/pretrain_synthetic.py) that gives a
+        # trained-like bimodal logit distribution; "structured" = the untrained seeded weights with
+        # the out_conv bias re-centred so that ~10% of each field's pixels pass its threshold.
+        self.sd = {k: torch.from_numpy(np.asarray(v)) for k, v in syn.make_state_dict(0, C, 3, args.weights).items()}
+        self.model = self.make_model(args.dtype)
+        self.world = world
+        self.stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def make_model(self, dtype):
+        from unet_mi355x.model import UNet
+        m = UNet(self.args.channels, 3, compute_dtype=dtype)
+        m.load_state_dict(self.sd)
+        return m.to(self.dev).eval()
+
+    def recentre(self, x):
+        """'structured' weights: shift the out_conv bias so ~10 % of each field passes (all ranks equal)."""
+        with torch.no_grad():   # full-batch forward: every profiled dispatch has the timed shape
+            lg = self.model(x)[:2]
+        thr = torch.tensor([0.25, 0.40, 0.30], dtype=torch.float64)
+        q = torch.quantile(lg.double().transpose(0, 1).reshape(3, -1).cpu(), 0.9, dim=1)
+        del lg
+        shift = (torch.log(thr / (1 - thr)) - q).float()
+        if self.world > 1:
+            shift = shift.to(self.dev)
+            dist.broadcast(shift, 0)
+            shift = shift.cpu()
+        with torch.no_grad():
+            self.model.out_conv.bias.add_(shift.to(self.dev))
+        self.sd = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+
+    def handle(self, model=None):
+        return (model or self.model).native_handle(self.dev)
+
+    def reserve(self, n, s, model=None):
+        self.handle(model).reserve(n, s, s)
+
+    def segment_fn(self, model=None):
+        h, stream, bits = self.handle(model), self.stream, self.native.MASK_BITS
+
+        def segment(x_local, masks_local):
+            h.forward(x_local, None, masks_local, bits, stream)
+        return segment
+
+
+class StandinRunner:
+    """CPU stand-in for the per-rank forward (tests/test_dist_cpu.py drives bench.py with it under
+    gloo): a deterministic function of each image into the bit-packed mask shape."""
+
+    def __init__(self, args, dev, world):
+        self.dev, self.world = dev, world
+
+    def reserve(self, n, s, model=None):
+        pass
+
+    def segment_fn(self, model=None):
+        def segment(x_local, masks_local):
+            v = x_local.sum(dim=(1, 2, 3)).abs().floor().to(torch.uint8)
+            masks_local.copy_((v.view(-1, 1, 1, 1) + torch.arange(masks_local.shape[-1], dtype=torch.uint8)
+                               ).expand_as(masks_local))
+        return segment
+
+
+def make_leg(runner, rank, world, n_total, per_rank, seed, S, C, dev, chunk):
+    """Buffers of one timed configuration on this rank: its input shard, its mask shard inside the
+    preallocated all-gather send buffer, and the step function (forward + the one exchange).  A
+    shard larger than ``chunk`` images runs as consecutive forwards of at most ``chunk`` (the
+    workspace is sized for ``chunk``: 194 MB per 512^2 image at 16 bits)."""
+    if per_rank is not None:                        # weak scaling: every rank holds per_rank images
+        lo, hi = rank * per_rank, (rank + 1) * per_rank
+        n_total = world * per_rank
+    else:
+        lo, hi = udist.shard_bounds(n_total, rank, world)
+    n_local = hi - lo
+    x = torch.from_numpy(gen_pages(seed + rank, max(n_local, 1), S, C)).to(dev)[:n_local]
+    gather = udist.MaskGather(n_total, (3, S, S // 8), torch.uint8, dev, rank=rank, world=world)
+    segment = runner.segment_fn()
+
+    def step():
+        for i in range(0, n_local, chunk):
+            segment(x[i:i + chunk], gather.local[i:i + chunk])
+        if world > 1:
+            gather()
+    return {"x": x, "gather": gather, "step": step, "n_total": n_total, "n_local": n_local}
+
+
+def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
+    """The bench contract's timing loop (udist.timed_steps): barrier + sync on both sides, the MAX
+    over ranks; optional per-step GPU times (HIP events on this stream) as a diagnostic."""
+    for _ in range(warmup):
+        leg["step"]()
+    ev = None
+    if per_step_events:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    marks = iter(ev[1:]) if ev else iter(())
+
+    def timed_step():
+        leg["step"]()
+        e = next(marks, None)
+        if e is not None:
+            e.record()
+    if ev:
+        sync()
+        ev[0].record()
+    elapsed, host = udist.timed_steps(timed_step, steps, 0, sync=sync, device=dev)
+    out = {"elapsed": elapsed, "ms_per_step": 1e3 * elapsed / steps,
+           "value": leg["n_total"] * steps / elapsed, "host_step_ms": [round(1e3 * t, 3) for t in host]}
+    if ev:
+        out["step_ms"] = [round(ev[i].elapsed_time(ev[i + 1]), 3) for i in range(steps)]
+    return out
+
+
+# ----------------------------------------------------------------------------- measurement legs
+def kernel_table(runner, model, x, masks, B, S, C, dtype, traffic_json):
+    """Per-launch HIP-event timing (unet_forward_timed, on the launch stream) -> per-instantiation
+    totals and the dominant kernel's roofline."""
+    native = runner.native
+    h = runner.handle(model)
+    labels = h.launch_labels()
+    ms = h.forward_timed(x, None, masks, native.MASK_BITS, runner.stream)
+    esize = 4 if dtype == "fp32" else 2
+    kernels, layer_ms = {}, {}
+    for (layer, lab, f, b, own), t in zip(launch_table(labels, B, S, S, C, esize), ms):
+        layer_ms[layer] = round(t, 3)
+        k = kernels.setdefault(lab, {"launches": 0, "ms": 0.0, "gflop": 0.0, "algo_gb": 0.0, "layers": []})
+        k["launches"] += 1 if own else 0
+        k["ms"] += t
+        k["gflop"] += f / 1e9
+        k["algo_gb"] += b / 1e9
+        k["layers"].append(layer)
+        if not own:   # issues no dispatch of its own (tools/pmc_summary.py)
+            k.setdefault("fused_layers", []).append(layer)
+    dom_name, dom = max(((n, k) for n, k in kernels.items() if k["gflop"] > 0 and "first_conv" not in n),
+                        key=lambda kv: kv[1]["ms"])
+    achieved = dom["gflop"] / dom["ms"]   # TFLOP/s (GFLOP / ms)
+    for k in kernels.values():
+        k["tflops"] = round(k["gflop"] / k["ms"], 1) if k["ms"] > 0 else None
+        k["algo_gbs"] = round(k["algo_gb"] / k["ms"] * 1e3, 1) if k["ms"] > 0 else None
+        k["avg_launch_ms"] = round(k["ms"] / max(1, k["launches"]), 4)
+        k["ms"] = round(k["ms"], 3)
+        k["gflop"] = round(k["gflop"], 1)
+        k["algo_gb"] = round(k["algo_gb"], 3)
+    peak = PEAK_TFLOPS[dtype]
+    traffic, source = None, None
+    if traffic_json == "auto":
+        traffic_json = os.path.join(REPO, "profiles", f"pmc_{dtype}_bs{B}.json")
+    if traffic_json and os.path.exists(traffic_json) and S == 512:
+        tj = json.load(open(traffic_json))
+        traffic = tj.get(dom_name, {}).get("hbm_bytes_per_launch")
+        meta = tj.get("_meta", {})
+        source = {"file": os.path.relpath(traffic_json, REPO), "commit": meta.get("source_commit"),
+                  "collected": meta.get("collected")}
+    roofline = {"bound": "mfma", "kernel": dom_name, "symbol": mangled(dom_name),
+                "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": source,
+                "launches_per_step": dom["launches"], "avg_launch_ms": dom["avg_launch_ms"],
+                "gflop_per_launch": round(dom["gflop"] / dom["launches"], 1),
+                "algo_bytes_per_launch": round(dom["algo_gb"] * 1e9 / dom["launches"])}
+    total_gflop = sum(launch_flops(e, B, S, S, C) for e in LAUNCHES) / 1e9
+    return kernels, layer_ms, roofline, total_gflop, sum(ms)
+
+
+def cpu_baseline(args, sd, x, masks, C, S):
     """The oracle (fp32 eager torch restating unet_model.py / inference.py) on this host's
     cores: batch-1 forward (images/s + the mask IoU of the GPU masks), batch-8 forward, and
     run_unet end to end (model load + resize + forward + masks + crops, inference.py:50-129)."""
@@ -164,7 +421,7 @@ def cpu_baseline(args, model, x, masks, C, S):
     from oracle import unet_oracle as orc
     threads, info = host_cores()
     torch.set_num_threads(threads)
-    sd_cpu = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    sd_cpu = {k: v.detach().cpu() for k, v in sd.items()}
     xc = x[:64].cpu()
     mk = np.unpackbits(masks[:64].cpu().numpy(), axis=-1, bitorder="little").astype(bool)
     orc.unet_forward(sd_cpu, xc[:1, :, :64, :64])  # warm the CPU kernels
@@ -203,59 +460,86 @@ def cpu_baseline(args, model, x, masks, C, S):
                            "images": done, "gpu_dtype": args.dtype}}
 
 
-def gpu_latency(args, model, dev):
-    """Batch-1 latency on the GPU: the drop-in run_unet (cached model, GPU preprocessing,
-    fused masks + boxes, host crops; inference.py:50-129) and the bare batch-1 forward,
-    eager (22 launches from the host) and as one hipGraph replay (unet_graph_launch)."""
+def fp32_leg(args, runner, dev):
+    """BASELINE config 2: a batch-32 512^2 fp32 forward on one GPU -- the reference's precision and
+    the drop-in's default (unet_mi355x/model.py DEFAULT_DTYPE) -- timed like the headline (HIP
+    events per launch for the roofline against the 157.3 TF fp32 MFMA peak)."""
+    B, S, C = args.fp32_batch, 512, args.channels
+    model = runner.make_model("fp32")
+    runner.reserve(B, S, model)
+    x = torch.from_numpy(gen_pages(2000, B, S, C)).to(dev)
+    masks = torch.empty((B, 3, S, S // 8), dtype=torch.uint8, device=dev)
+    seg = runner.segment_fn(model)
+    leg = {"step": lambda: seg(x, masks), "n_total": B}
+    t = time_leg(leg, args.fp32_steps, 2, torch.cuda.synchronize, dev)
+    kernels, layer_ms, roof, gflop, _ = kernel_table(runner, model, x, masks, B, S, C, "fp32", "auto")
+    out = {"config": f"BASELINE config 2 shape: batch {B}, {S}x{S}, UNet({C},3), fp32 storage + exact-fp32 MFMA "
+                     "(v_mfma_f32_16x16x4_f32), fused bit-packed masks",
+           "value": round(t["value"], 2), "unit": "images/s", "ms_per_step": round(t["ms_per_step"], 3),
+           "steps": args.fp32_steps, "whole_step_tflops": round(gflop / t["ms_per_step"], 1),
+           "roofline": roof, "kernels": kernels, "layer_ms": layer_ms}
+    model.close()
+    del x, masks
+    return out
+
+
+def gpu_latency(args, runner, dev):
+    """Batch-1 latency on the GPU at the drop-in default (fp32) and at the bench plan: the drop-in
+    run_unet (cached model, GPU preprocessing, fused masks + boxes, host crops; inference.py:50-129)
+    and the bare batch-1 forward, eager (22 launches from the host) and as one hipGraph replay."""
     from PIL import Image
     from unet_mi355x import inference as inf
-    out = {}
+    native = runner.native
     page = syn.invoice_pages(7, 1, 400, 600, 1)[0, 0]
     pil = Image.fromarray((np.stack([page, page * 0.97, page * 0.94], -1) * 255 + 0.5).astype(np.uint8), "RGB")
-    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     inf.DEVICE = str(dev)
+    res = {}
     with tempfile.TemporaryDirectory() as td:
         ck = os.path.join(td, "best_unet_model.pth")
-        torch.save(sd, ck)
-        t0 = time.perf_counter()
-        inf.run_unet(pil, ck, compute_dtype=args.dtype)
-        out["run_unet_first_call_ms"] = round(1e3 * (time.perf_counter() - t0), 2)
-        lat = []
-        for _ in range(20):
+        torch.save(runner.sd, ck)
+        for dtype in dict.fromkeys(("fp32", args.dtype)):
+            out = res[dtype] = {}
             t0 = time.perf_counter()
-            inf.run_unet(pil, ck, compute_dtype=args.dtype)
-            lat.append(time.perf_counter() - t0)
-        out["run_unet_ms"] = round(1e3 * float(np.median(lat)), 3)
-    h = model.native_handle(dev)
-    x1 = torch.from_numpy(gen_pages(3, 1, 512, 3)).to(dev)
-    m1 = torch.empty((1, 3, 512, 64), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    h.reserve(1, 512, 512)
-    for _ in range(3):
-        h.forward(x1, None, m1, native.MASK_BITS, stream)
-    torch.cuda.synchronize()
-    ref = m1.clone()
-    reps = 50
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        h.forward(x1, None, m1, native.MASK_BITS, stream)
-    e1.record()
-    torch.cuda.synchronize()
-    out["forward_bs1_eager_ms"] = round(e0.elapsed_time(e1) / reps, 4)
-    g = h.graph(x1, None, m1, native.MASK_BITS)
-    m1.zero_()
-    g.launch(stream)
-    torch.cuda.synchronize()
-    out["graph_matches_eager"] = bool(torch.equal(m1, ref))
-    e0.record()
-    for _ in range(reps):
-        g.launch(stream)
-    e1.record()
-    torch.cuda.synchronize()
-    out["forward_bs1_graph_ms"] = round(e0.elapsed_time(e1) / reps, 4)
-    g.close()
-    return out
+            inf.run_unet(pil, ck, compute_dtype=dtype)
+            out["run_unet_first_call_ms"] = round(1e3 * (time.perf_counter() - t0), 2)
+            lat = []
+            for _ in range(20):
+                t0 = time.perf_counter()
+                inf.run_unet(pil, ck, compute_dtype=dtype)
+                lat.append(time.perf_counter() - t0)
+            out["run_unet_ms"] = round(1e3 * float(np.median(lat)), 3)
+            model = inf._cached_model(ck, dtype)
+            h = model.native_handle(dev)
+            x1 = torch.from_numpy(gen_pages(3, 1, 512, 3)).to(dev)
+            m1 = torch.empty((1, 3, 512, 64), dtype=torch.uint8, device=dev)
+            h.reserve(1, 512, 512)
+            for _ in range(3):
+                h.forward(x1, None, m1, native.MASK_BITS, runner.stream)
+            torch.cuda.synchronize()
+            ref = m1.clone()
+            reps = 50
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                h.forward(x1, None, m1, native.MASK_BITS, runner.stream)
+            e1.record()
+            torch.cuda.synchronize()
+            out["forward_bs1_eager_ms"] = round(e0.elapsed_time(e1) / reps, 4)
+            g = h.graph(x1, None, m1, native.MASK_BITS)
+            m1.zero_()
+            g.launch(runner.stream)
+            torch.cuda.synchronize()
+            out["graph_matches_eager"] = bool(torch.equal(m1, ref))
+            e0.record()
+            for _ in range(reps):
+                g.launch(runner.stream)
+            e1.record()
+            torch.cuda.synchronize()
+            out["forward_bs1_graph_ms"] = round(e0.elapsed_time(e1) / reps, 4)
+            out["run_unet_over_forward"] = round(out["run_unet_ms"] / out["forward_bs1_eager_ms"], 3)
+            g.close()
+        inf._cache.clear()
+    return res
 
 
 def main():
@@ -263,7 +547,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="images per step over all ranks (strong scaling; overrides --batch)")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--channels", type=int, default=3)
     ap.add_argument("--dtype", default="mixed", choices=["mixed", "bf16", "fp16", "fp32"])
@@ -272,149 +558,105 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-layer-profile", action="store_true")
+    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling shapes (global 256 / 1024)")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 config-2 leg")
+    ap.add_argument("--fp32-batch", type=int, default=32)
+    ap.add_argument("--fp32-steps", type=int, default=5)
+    ap.add_argument("--standin", action="store_true",
+                    help="CPU stand-in forward over gloo (tests: the launcher, sharding and timing without a GPU)")
     ap.add_argument("--traffic-json", default="auto",
                     help="PMC summary (tools/pmc_summary.py output) to fill roofline.traffic; 'auto' = "
                          "profiles/pmc_<dtype>_bs<batch>.json when present (collected by tools/gpu_round.sh)")
     args = ap.parse_args()
 
+    # ---- launch: one process per GPU.  Self-spawn before any GPU call when not under torchrun.
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        if not args.standin and torch.cuda.device_count() < args.gpus:   # device_count initialises no GPU
+            print(f"bench: --gpus {args.gpus} but only {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+            sys.exit(2)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    if "RANK" in os.environ and "MASTER_ADDR" in os.environ:   # launched by torchrun
-        dist.init_process_group("nccl", device_id=dev)          # RCCL over xGMI
-    if args.gpus != world and rank == 0:
-        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a different GPU count",
+              file=sys.stderr)
+        sys.exit(2)
+    if args.standin:
+        dev = torch.device("cpu")
+        sync = lambda: None  # noqa: E731
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        runner = StandinRunner(args, dev, world)
+    else:
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        sync = torch.cuda.synchronize
+        if world > 1:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)   # RCCL over xGMI
+        runner = NativeRunner(args, dev, world)
 
-    B, S, C = args.batch, args.size, args.channels
-    # weights: the real checkpoint is an LFS pointer, so the seeded synthetic weights with the
-    # fine-tuned BN/bias subset ("pretrained", tools/pretrain_synthetic.py) that gives a
-    # trained-like bimodal logit distribution; "structured" = the untrained seeded weights with
-    # the out_conv bias re-centred so that ~10% of each field's pixels pass its threshold.
-    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in syn.make_state_dict(0, C, 3, args.weights).items()}
-    model = UNet(C, 3, compute_dtype=args.dtype)
-    model.load_state_dict(sd)
-    model = model.to(dev).eval()
-    x = torch.from_numpy(gen_pages(1000 + rank, B, S, C)).to(dev)
-    if args.weights == "structured":
-        with torch.no_grad():   # full-batch forward: every profiled dispatch has the timed shape
-            lg = model(x)[:2]
-        thr = torch.tensor([0.25, 0.40, 0.30], dtype=torch.float64)
-        q = torch.quantile(lg.double().transpose(0, 1).reshape(3, -1).cpu(), 0.9, dim=1)
-        del lg
-        shift = (torch.log(thr / (1 - thr)) - q).float()
-        if world > 1:   # identical weights on every rank
-            shift = shift.to(dev)
-            dist.broadcast(shift, 0)
-            shift = shift.cpu()
-        with torch.no_grad():
-            model.out_conv.bias.add_(shift.to(dev))
-    handle = model.native_handle(dev)
-    handle.reserve(B, S, S)
+    if os.environ.get("BENCH_FAIL_RANK") == str(rank):   # tests: a rank dying must fail the whole job
+        print(f"bench: rank {rank} failing on request (BENCH_FAIL_RANK)", file=sys.stderr)
+        sys.exit(3)
+    S, C = args.size, args.channels
+    strong = args.global_batch is not None
+    legs_cfg = [("main", args.global_batch if strong else None, None if strong else args.batch)]
+    if not args.no_strong and S == 512:
+        legs_cfg += [(f"strong_{g}", g, None) for g in STRONG_GLOBAL if not (strong and g == args.global_batch)]
+    chunk = max(args.batch, udist.shard_bounds(args.global_batch, 0, world)[1]) if strong else args.batch
+    runner.reserve(chunk, S)
 
-    masks = torch.empty((B, 3, S, S // 8), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    main_leg = make_leg(runner, rank, world, args.global_batch, None if strong else args.batch, 1000, S, C, dev,
+                        chunk)
+    B = main_leg["n_local"]
+    if not args.standin and args.weights == "structured":
+        runner.recentre(main_leg["x"])
+    res = time_leg(main_leg, args.steps, args.warmup, sync, dev, per_step_events=not args.standin)
 
-    def segment(x_local, masks_local):
-        handle.forward(x_local, None, masks_local, native.MASK_BITS, stream)
-
-    def step():
-        if world > 1:   # this rank's shard + the one exchange step: RCCL all-gather of the masks
-            udist.sharded_mask_step(segment, x, masks, world * B)
-        else:
-            segment(x, masks)
-
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]   # per-step spread (diagnostic)
-    marks = iter(ev[1:])
-
-    def timed_step():
-        step()
-        e = next(marks, None)
-        if e is not None:
-            e.record()
-
-    for _ in range(args.warmup):
-        step()
-    ev[0].record()
-    elapsed, _ = udist.timed_steps(timed_step, args.steps, 0, sync=torch.cuda.synchronize, device=dev)
-    ms_per_step = 1e3 * elapsed / args.steps
-    step_ms = [round(ev[i].elapsed_time(ev[i + 1]), 3) for i in range(args.steps)]
-    value = world * B * args.steps / elapsed
+    # ---- strong-scaling shapes (same timing protocol, fewer steps)
+    strong_out = []
+    for name, g, _ in legs_cfg[1:]:
+        leg = make_leg(runner, rank, world, g, None, 3000, S, C, dev, chunk)
+        t = time_leg(leg, min(args.steps, 10), 2, sync, dev)
+        strong_out.append({"global_batch": g, "per_rank_batch": leg["n_local"] if world == 1 else
+                           [udist.shard_bounds(g, r, world)[1] - udist.shard_bounds(g, r, world)[0] for r in range(world)],
+                           "value": round(t["value"], 2), "ms_per_step": round(t["ms_per_step"], 3),
+                           "steps": min(args.steps, 10)})
+        del leg
 
     # ---- per-launch HIP-event timing (same stream) -> dominant kernel roofline
-    kernels, roofline, layer_ms = {}, None, {}
-    if not args.no_layer_profile:
-        labels = handle.launch_labels()
-        ms = handle.forward_timed(x, None, masks, native.MASK_BITS, stream)
-        esize = 4 if args.dtype == "fp32" else 2
-        prev = None
-        for entry, lab, t in zip(LAUNCHES, labels, ms):
-            layer_ms[entry[0]] = round(t, 3)
-            fused = not lab   # a launch slot fused into the previous launch (up1 into conv2.3)
-            if fused:
-                lab = prev
-            k = kernels.setdefault(lab, {"launches": 0, "ms": 0.0, "gflop": 0.0, "algo_gb": 0.0, "layers": []})
-            k["launches"] += 0 if fused else 1
-            k["ms"] += t
-            k["gflop"] += launch_flops(entry, B, S, S, C) / 1e9
-            gb = launch_bytes(entry, B, S, S, C, esize) / 1e9
-            if fused:   # its input is the previous launch's output, never written to HBM: minus both trips
-                _, cin, _, lvl, _ = entry
-                gb -= 2 * B * (S >> lvl) * (S >> lvl) * cin * esize / 1e9
-            k["algo_gb"] += gb
-            k["layers"].append(entry[0])
-            if fused:   # issues no dispatch of its own (tools/pmc_summary.py)
-                k.setdefault("fused_layers", []).append(entry[0])
-            prev = lab
-        dom_name, dom = max(((n, k) for n, k in kernels.items() if "first_conv" not in n and "x_to_px4" not in n),
-                            key=lambda kv: kv[1]["ms"])
-        achieved = dom["gflop"] / dom["ms"]   # TFLOP/s (GFLOP / ms)
-        for k in kernels.values():
-            k["tflops"] = round(k["gflop"] / k["ms"], 1) if k["ms"] > 0 else None
-            k["algo_gbs"] = round(k["algo_gb"] / k["ms"] * 1e3, 1) if k["ms"] > 0 else None
-            k["avg_launch_ms"] = round(k["ms"] / k["launches"], 4)
-            k["ms"] = round(k["ms"], 3)
-            k["gflop"] = round(k["gflop"], 1)
-            k["algo_gb"] = round(k["algo_gb"], 2)
-        peak = PEAK_TFLOPS[args.dtype]
-        traffic = None
-        tj_path = args.traffic_json
-        if tj_path == "auto":
-            tj_path = os.path.join(REPO, "profiles", f"pmc_{args.dtype}_bs{B}.json")
-        if tj_path and os.path.exists(tj_path) and S == 512:
-            tj = json.load(open(tj_path))
-            traffic = tj.get(dom_name, {}).get("hbm_bytes_per_launch")
-        roofline = {"bound": "mfma", "kernel": dom_name, "symbol": mangled(dom_name),
-                    "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4), "traffic": traffic,
-                    "launches_per_step": dom["launches"], "avg_launch_ms": dom["avg_launch_ms"],
-                    "gflop_per_launch": round(dom["gflop"] / dom["launches"], 1),
-                    "algo_bytes_per_launch": round(dom["algo_gb"] * 1e9 / dom["launches"]),
-                    "whole_step_tflops": round(sum(launch_flops(e, B, S, S, C) for e in LAUNCHES) / 1e9 /
-                                               sum(ms), 1)}
+    kernels, roofline, layer_ms, whole = {}, None, {}, None
+    if not args.no_layer_profile and not args.standin and B > 0:
+        kernels, layer_ms, roofline, gflop, _ = kernel_table(runner, None, main_leg["x"], main_leg["gather"].local,
+                                                             B, S, C, args.dtype, args.traffic_json)
+        whole = round(gflop / (res["ms_per_step"]), 1)   # algorithmic TFLOP/s of the timed step
+        roofline["whole_step_tflops"] = whole
 
-    # ---- CPU baseline (the oracle, fp32 eager on this host), rank 0 at N=1 only
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, model, x, masks, C, S)
-    lat = None
-    if rank == 0 and world == 1 and not args.no_latency and S == 512 and C == 3:
-        lat = gpu_latency(args, model, dev)
+    # ---- rank 0 at N=1: fp32 config-2 leg, CPU baseline, batch-1 latency
+    fp32 = cpu = lat = None
+    solo = rank == 0 and world == 1 and not args.standin
+    if solo and not args.no_fp32 and S == 512 and args.dtype != "fp32":
+        fp32 = fp32_leg(args, runner, dev)
+    if solo and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, runner.sd, main_leg["x"], main_leg["gather"].local, C, S)
+    if solo and not args.no_latency and S == 512 and C == 3:
+        lat = gpu_latency(args, runner, dev)
 
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "metric": METRIC, "value": round(res["value"], 2), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(res["ms_per_step"], 3),
+            "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "bf16+fp16" if args.dtype == "mixed" else args.dtype,
             "data": f"synthetic (seeded invoice-like pages, gray x3; '{args.weights}' seeded weights -- "
-                    "the trained checkpoint is an LFS pointer)",
+                    "the trained checkpoint is an LFS pointer)" if not args.standin else "standin (CPU, gloo)",
             "config": {"workload": f"UNet(n_channels={C}, n_classes=3) forward {S}x{S} + fused sigmoid/"
                                    f"threshold bit-packed masks" + (" + RCCL all-gather" if world > 1 else ""),
-                       "global_batch": world * B, "per_gpu_batch": B, "image": S,
+                       "global_batch": main_leg["n_total"], "per_gpu_batch": B, "image": S,
                        "parallelism": f"dp{world}", "precision_plan": PLAN[args.dtype]},
-            "roofline": roofline, "cpu_baseline": cpu, "latency_bs1": lat, "step_ms": step_ms,
+            "roofline": roofline, "cpu_baseline": cpu, "strong_scaling": strong_out, "fp32": fp32,
+            "latency_bs1": lat, "step_ms": res.get("step_ms"), "host_step_ms": res["host_step_ms"],
             "kernels": kernels, "layer_ms": layer_ms,
         }
         print(json.dumps(out), flush=True)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 1
+#define UNET_ABI_VERSION 2   /* 2: unet_forward requires unet_reserve; Cfg renumbered; fp16 range check */
 
 /* error codes */
 #define UNET_OK 0
@@ -48,7 +48,10 @@ extern "C" {
 #define UNET_DTYPE_BF16 1
 #define UNET_DTYPE_F16 2
 /* bf16 at resolution levels 2-4, fp16 at the two full-resolution levels 0-1 (where the mask
- * boundaries are decided): the precision plan of the headline benchmark, see DESIGN.md §2 */
+ * boundaries are decided): the precision plan of the headline benchmark, see DESIGN.md §2.
+ * fp16 storage (UNET_DTYPE_F16, and levels 0-1 of MIXED) holds |v| <= 65504: unet_load_weights
+ * refuses (UNET_EINVAL) a checkpoint whose BN-folded weights or biases exceed that at an fp16
+ * level; activations beyond it would become inf -- use BF16 (fp32's range) or F32 for such nets. */
 #define UNET_DTYPE_MIXED 3
 
 /* input layouts / dtypes accepted by unet_forward */
@@ -93,8 +96,11 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* tensors, int n);
 size_t unet_workspace_bytes(const unet_handle* h, int N, int H, int W);
 
 /* Allocate (grow) the workspace for up to (N, H, W): unet_forward requires it (UNET_ESTATE
- * otherwise) and then neither allocates nor synchronises (graph-capturable).  Growing waits for
- * the handle's queued work. */
+ * otherwise; ABI 1 allocated inside the forward) and then neither allocates nor synchronises
+ * (graph-capturable).  Growing waits for the handle's queued work.
+ * A forward issued on a stream under capture (unet_graph_create, or the caller's own capture, e.g.
+ * torch.cuda.graph on its side stream) neither waits for nor records the handle's stream-order
+ * event; ordering the replay after other work on the handle is then the caller's. */
 int unet_reserve(unet_handle* h, int N, int H, int W);
 
 /* Forward pass.  x: device tensor [N][n_channels][H][W] (x_layout UNET_LAYOUT_NCHW) or

@@ -211,6 +211,9 @@ def test_batch256_bench_shape_invariance_and_iou():
         full = m.forward_masks(x, packed=True).clone()
         half = m.forward_masks(x[128:].contiguous(), packed=True)
     assert torch.equal(half, full[128:]), "N=128 shard differs from the N=256 batch"
+    with torch.no_grad():   # rank 1's shard of global batch 256 over 8 GPUs (the strong-scaling shape)
+        eighth = m.forward_masks(x[32:64].contiguous(), packed=True)
+    assert torch.equal(eighth, full[32:64]), "N=32 shard differs from the N=256 batch"
     sample = [0, 77, 128, 255]
     ious = []
     for i in sample:
@@ -341,6 +344,8 @@ def test_rccl_allgather_c_abi_single_rank():
     h.allgather(masks, out, stream)
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+    with pytest.raises(ValueError, match="recv"):   # a short recv buffer is refused, not overrun
+        h.allgather(masks, out[:1], stream)
     h.comm_destroy()
     m.close()
 
@@ -367,6 +372,80 @@ def test_u8_nhwc_input_equals_f32_nchw():
         torch.cuda.synchronize()
         assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), dtype
         m.close()
+
+
+def test_u8_nhwc_input_with_unfused_first_layer(monkeypatch):
+    """a 16-bit handle whose down1.3 is overridden to a non-fused configuration converts
+    a uint8 NHWC input to fp32 NCHW (12 B per pixel) inside the workspace; the buffer must hold it
+    (it was sized 8 B per pixel) and the result must equal the fp32 NCHW input's bitwise."""
+    monkeypatch.setenv("UNET_MI355X_CFG", "0:10")   # CFG_RING8_R64_WS: the unfused weight-stationary ring
+    rng = np.random.default_rng(6)
+    u8 = rng.integers(0, 256, (3, 64, 96, 3), dtype=np.uint8)
+    f32 = np.ascontiguousarray((u8.astype(np.float32) / np.float32(255.0)).transpose(0, 3, 1, 2))
+    sd = syn.make_state_dict(0, 3, 3, profile="structured")
+    m = make_model(sd, 3, "mixed")
+    h = m.native_handle(torch.device(DEV))
+    assert not h.launch_labels()[0].startswith("x_to_px4")
+    stream = torch.cuda.current_stream().cuda_stream
+    h.reserve(3, 64, 96)
+    lg = [torch.empty((3, 3, 64, 96), device=DEV) for _ in range(2)]
+    h.forward(torch.from_numpy(u8).to(DEV), lg[0], None, native.MASK_NONE, stream, layout=native.LAYOUT_NHWC)
+    h.forward(torch.from_numpy(f32).to(DEV), lg[1], None, native.MASK_NONE, stream)
+    torch.cuda.synchronize()
+    assert torch.equal(lg[0], lg[1])
+    ref = orc.unet_forward(sd, torch.from_numpy(f32)).numpy()
+    assert rel_err(lg[0].cpu().numpy(), ref) <= TOL["mixed"]
+    m.close()
+
+
+def test_fp16_range_refused_at_load():
+    """fp16 storage holds |v| <= 65504.  A checkpoint whose BN fold leaves a conv weight
+    beyond that at an fp16 level (here a running_var of 1e-12 at down1.3: scale ~316 x gamma) is
+    refused by the fp16 / mixed plans (ValueError) instead of producing inf; bf16 and fp32 load it."""
+    sd = syn.make_state_dict(0, 3, 3, profile="structured")
+    sd["down1.net.4.weight"] = np.full_like(np.asarray(sd["down1.net.4.weight"]), 1e5)
+    sd["down1.net.4.running_var"] = np.full_like(np.asarray(sd["down1.net.4.running_var"]), 1e-12)
+    x = torch.from_numpy(syn.uniform_batch(1, 1, 3, 32, 32)).to(DEV)
+    for dtype in ("fp16", "mixed"):
+        m = make_model(sd, 3, dtype)
+        with pytest.raises(ValueError, match="fp16 range"), torch.no_grad():
+            m(x)
+        m.close()
+    for dtype in ("bf16", "fp32"):
+        m = make_model(sd, 3, dtype)
+        with torch.no_grad():
+            m(x)
+        m.close()
+
+
+def test_torch_graph_capture_on_side_stream():
+    """torch.cuda.graph captures on its own side stream, after eager forwards on the
+    default stream; the library must not wait on (or record) its stream-order event inside the
+    capture.  The replayed masks equal the eager ones."""
+    sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
+    m = make_model(sd, 3, "mixed")
+    x = torch.from_numpy(syn.invoice_pages(61, 2, 256, 256, 3)).to(DEV)
+    m.reserve(2, 256, 256)
+    with torch.no_grad():
+        ref = m.forward_masks(x, packed=True).clone()       # eager, default stream: the event is pending
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                m.forward_masks(x, packed=True)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = m.forward_masks(x, packed=True)
+        out.zero_()
+        for _ in range(2):
+            g.replay()
+        torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    with torch.no_grad():   # the handle is usable eagerly afterwards
+        assert torch.equal(m.forward_masks(x, packed=True), ref)
+    del g
+    m.close()
 
 
 def test_bf16_cast_model_loads():
@@ -398,14 +477,24 @@ def test_errors_and_no_fallback():
 
 
 def test_weight_update_repacks():
+    """Parameter changes re-pack the handle: in-place updates, a replaced Parameter object, and a
+    .to() round trip (the cached signature tensors are rebuilt on re-registration / conversion)."""
     sd = syn.make_state_dict(4, 3, 3)
     m = make_model(sd, 3, "fp32")
     x = torch.from_numpy(syn.uniform_batch(1, 1, 3, 32, 32)).to(DEV)
     with torch.no_grad():
         a = m(x).clone()
         m.out_conv.bias.add_(1.0)
-        b = m(x)
+        b = m(x).clone()
+        m.out_conv.bias = torch.nn.Parameter(m.out_conv.bias.detach() + 1.0)
+        c = m(x).clone()
+        m.to("cpu")
+        m.out_conv.bias.add_(1.0)
+        m.to(DEV)
+        d = m(x)
     assert torch.allclose(b - a, torch.ones_like(a), atol=1e-4)
+    assert torch.allclose(c - b, torch.ones_like(a), atol=1e-4)
+    assert torch.allclose(d - c, torch.ones_like(a), atol=1e-4)
     m.close()
 
 
@@ -663,13 +752,22 @@ def test_run_unet_boundary_matches_reference_golden():
         iou = orc.mask_iou(masks[k], ref)
         print(f"run_unet {k}: IoU {iou:.6f}, differing pixels {int((masks[k] != ref).sum())}")
         assert iou >= 0.999
+        # the crop rules (inference.py:92-127) applied to the box of the REFERENCE's mask reproduce
+        # its crop byte for byte; our own crop must too whenever our mask has the same box (a mask
+        # pixel off inside the box changes nothing downstream)
+        ref_box = inf.mask_box(ref)
+        from_ref = inf.crop_from_box(pil, ref_box)
         if bool(z["crop_none_" + k]):
-            assert crops[k] is None
+            assert crops[k] is None and from_ref is None
+            continue
+        want = str(z["crop_sha256_" + k])
+        assert hashlib.sha256(np.asarray(from_ref).tobytes()).hexdigest() == want
+        arr = np.asarray(crops[k])
+        assert list(arr.shape) == list(z["crop_shape_" + k])
+        if inf.mask_box(masks[k]) == ref_box:
+            assert hashlib.sha256(arr.tobytes()).hexdigest() == want, k
         else:
-            arr = np.asarray(crops[k])
-            assert list(arr.shape) == list(z["crop_shape_" + k])
-            if np.array_equal(masks[k], ref):
-                assert hashlib.sha256(arr.tobytes()).hexdigest() == str(z["crop_sha256_" + k])
+            print(f"run_unet {k}: box {inf.mask_box(masks[k])} vs reference {ref_box}")
 
 
 def test_run_unet_batch_equals_per_photo_calls():

@@ -53,7 +53,7 @@ def load_pass(d):
 
 
 def main():
-    from bench import LAUNCHES, launch_bytes, launch_flops
+    from bench import LAUNCHES, launch_table
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--batch", type=int, default=256)
@@ -61,14 +61,17 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--esize", type=int, default=2)
     ap.add_argument("--bench-json", default=None,
-                    help="bench.py JSON line of the same build: launches it reports as fused_into_* issue no dispatch")
+                    help="bench.py JSON line of the same build: launches it reports as fused_layers issue no dispatch")
+    ap.add_argument("--commit", default=None, help="git commit of the profiled tree (stamped into _meta)")
     a = ap.parse_args()
-    launches = list(LAUNCHES)
+    labels = ["?"] * len(LAUNCHES)
     if a.bench_json:
         kern = json.loads(open(a.bench_json).read().strip().splitlines()[-1])["kernels"]
-        fused = {l for k, v in kern.items() if k.startswith("fused_into") for l in v["layers"]}
-        fused |= {l for v in kern.values() for l in v.get("fused_layers", [])}   # e.g. up1 inside conv2.3
-        launches = [e for e in LAUNCHES if e[0] not in fused]
+        by_layer = {l: k for k, v in kern.items() for l in v["layers"]}
+        fused = {l for v in kern.values() for l in v.get("fused_layers", [])}   # e.g. up1 inside conv2.3
+        labels = ["" if e[0] in fused else by_layer.get(e[0], "?") for e in LAUNCHES]
+    table = launch_table(labels, a.batch, a.size, a.size, 3, a.esize)
+    launches = [r for r in table if r[4]]    # the slots that issue a dispatch
     per_launch = [dict() for _ in launches]
     for p in sorted(glob.glob(os.path.join(a.dir, "pass*"))):
         if not os.path.isdir(p):
@@ -84,10 +87,7 @@ def main():
             per_launch[i]["kernel_name"] = name
     print(f"{'launch':14s} {'read_GB':>8s} {'write_GB':>8s} {'algo_GB?':>8s} {'mfma_busy%':>10s} {'lds_conf%':>9s} {'wait_any%':>9s}")
     agg = defaultdict(lambda: defaultdict(float))
-    labels = {}
-    if a.bench_json:
-        labels = {l: k for k, v in kern.items() for l in v["layers"]}
-    for e, c in zip(launches, per_launch):
+    for (layer, lab, flops, algo, _), c in zip(launches, per_launch):
         rd = 2 * c.get("FETCH_SIZE", 0) * 1024
         wr = c.get("WRITE_SIZE", 0) * 1024
         busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0)
@@ -95,15 +95,16 @@ def main():
         mfma_pct = 100 * busy / (gui / 8 * 256 * 4) if gui else 0   # per-SIMD busy over (cycles x 1024 SIMDs)
         conf = 100 * c.get("SQ_LDS_BANK_CONFLICT", 0) / max(1, c.get("SQ_LDS_IDX_ACTIVE", 0))
         wait = 100 * c.get("SQ_WAIT_ANY", 0) / max(1, c.get("SQ_WAVE_CYCLES", 0))
-        algo = launch_bytes(e, a.batch, a.size, a.size, 3, a.esize)
-        print(f"{e[0]:14s} {rd / 1e9:8.2f} {wr / 1e9:8.2f} {algo / 1e9:8.2f} {mfma_pct:10.1f} {conf:9.2f} {wait:9.1f}")
-        k = agg[labels.get(e[0]) or label_of(c.get("kernel_name", e[0]))]
+        print(f"{layer:14s} {rd / 1e9:8.2f} {wr / 1e9:8.2f} {algo / 1e9:8.2f} {mfma_pct:10.1f} {conf:9.2f} {wait:9.1f}")
+        k = agg[lab if lab not in ("", "?") else label_of(c.get("kernel_name", layer))]
         k["launches"] += 1
         k["hbm_read_bytes"] += rd
         k["hbm_write_bytes"] += wr
-        k["gflop"] += launch_flops(e, a.batch, a.size, a.size, 3) / 1e9
+        k["gflop"] += flops / 1e9
         k["algo_bytes"] += algo
-    out = {}
+    import time
+    out = {"_meta": {"source_commit": a.commit, "collected": time.strftime("%Y-%m-%d"), "dir": a.dir,
+                     "batch": a.batch, "size": a.size}}
     for name, k in agg.items():
         n = k["launches"]
         out[name] = {"launches": int(n), "hbm_bytes_per_launch": (k["hbm_read_bytes"] + k["hbm_write_bytes"]) / n,

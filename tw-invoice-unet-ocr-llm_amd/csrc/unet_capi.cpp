@@ -9,6 +9,7 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -218,8 +219,10 @@ Buffers plan(DType dt, int N, int H, int W) {
   o = align256(o + (size_t)kMaxClasses * P / 8);
   // network input in the first layer's format: T [N][H][W][4] (16-bit ring kernel's fused first
   // conv) or fp32 NCHW (fp32 path, when the caller's input is not fp32 NCHW already)
+  // (either buffer of the two: 8 B per pixel for T [N][H][W][4], up to 12 B for fp32 NCHW with C = 3
+  // -- the latter also on a 16-bit plan whose down1.3 is overridden to a non-fused configuration)
   b.xpx = o;
-  o = align256(o + P * (e == 2 ? 4 * 2 : 3 * 4));
+  o = align256(o + P * 3 * 4);
   b.total = o;
   return b;
 }
@@ -286,6 +289,20 @@ void put_elem(DType dt, std::vector<uint8_t>& buf, size_t idx, double v) {
     uint16_t u = dt == DType::BF16 ? f32_to_bf16((float)v) : f32_to_f16((float)v);
     std::memcpy(&buf[idx * 2], &u, 2);
   }
+}
+
+// fp16 storage (the fp16 and mixed plans) holds |v| <= 65504: a folded weight or bias beyond that
+// (e.g. a BatchNorm with a tiny running_var: scale gamma / sqrt(var + 1e-5) up to ~316 gamma) would
+// silently become inf.  Refused at load time; bf16 keeps fp32's range.
+int check_f16_range(DType dt, const std::vector<double>& w, const std::vector<double>& b, const std::string& what) {
+  if (dt != DType::F16) return UNET_OK;
+  double m = 0.0;
+  for (double v : w) m = std::max(m, std::fabs(v));
+  for (double v : b) m = std::max(m, std::fabs(v));
+  if (!(m <= 65504.0))
+    return fail(UNET_EINVAL, what + ": folded weights reach " + std::to_string(m) +
+                                 ", beyond the fp16 range (65504) of this precision plan; use dtype bf16 or fp32");
+  return UNET_OK;
 }
 
 // 3x3 layer: packed[rho][tap*cin + c] = W'[nat(rho)][c][ky][kx], tap = ky*3+kx
@@ -375,11 +392,19 @@ int packT(unet_handle* h, Layer& L, const float* W, const float* B) {
 // Make the next use of the shared workspace (and of the preprocess buffers) on `s` wait for the
 // previous call if that ran on another stream; unet_forward / unet_preprocess calls on different
 // streams are thus serialised on the device, not only on the host (the handle has ONE workspace).
+// A stream under capture (unet_graph_create's own, or a caller's: torch.cuda.graph captures on a
+// side stream) records nothing and waits for nothing: an event recorded outside the capture must not
+// enter it, and the captured work runs only when the graph is launched (the caller orders that).
+bool stream_capturing(unet_handle* h, hipStream_t s) {
+  if (h->capturing) return true;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
 void order_after_last(unet_handle* h, hipStream_t s) {
-  if (!h->capturing && h->pending && h->last_stream != s) (void)hipStreamWaitEvent(s, h->done, 0);
+  if (h->pending && h->last_stream != s && !stream_capturing(h, s)) (void)hipStreamWaitEvent(s, h->done, 0);
 }
 void mark_done(unet_handle* h, hipStream_t s) {
-  if (!h->capturing && hipEventRecord(h->done, s) == hipSuccess) {
+  if (!stream_capturing(h, s) && hipEventRecord(h->done, s) == hipSuccess) {
     h->last_stream = s;
     h->pending = true;
   }
@@ -710,6 +735,7 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
   std::vector<double> w, b;
   const int C = h->cfg.n_channels;
   int rc = fold(sd, "down1", "0", C, 64, w, b);
+  if (!rc) rc = check_f16_range(h->L[D1B].dt, w, b, "down1.net.0");
   if (rc) return rc;
   {
     std::vector<float> wf(w.begin(), w.end()), bf(b.begin(), b.end());
@@ -756,6 +782,7 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
   }
   for (int i = 0; i < 17; ++i) {
     rc = fold(sd, kLayerKey[i][0], kLayerKey[i][1], h->L[i].cin, h->L[i].cout, w, b);
+    if (!rc) rc = check_f16_range(h->L[i].dt, w, b, std::string(kLayerKey[i][0]) + ".net." + kLayerKey[i][1]);
     if (!rc) rc = pack3x3(h, h->L[i], w, b);
     if (rc) return rc;
   }
@@ -765,7 +792,9 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
     const float* W = sd.get(std::string(kUpKey[i]) + ".weight", {L.cin, L.cout, 2, 2}, err);
     const float* B = W ? sd.get(std::string(kUpKey[i]) + ".bias", {L.cout}, err) : nullptr;
     if (!B) return fail(UNET_EKEY, err);
-    rc = packT(h, h->U[i], W, B);
+    rc = check_f16_range(L.dt, std::vector<double>(W, W + (size_t)L.cin * L.cout * 4), std::vector<double>(B, B + L.cout),
+                         kUpKey[i]);
+    if (!rc) rc = packT(h, h->U[i], W, B);
     if (rc) return rc;
     if (i == 3 && h->fuse_up1) {   // conv2.3 + up1 in one launch
       rc = fold(sd, kLayerKey[C2B][0], kLayerKey[C2B][1], h->L[C2B].cin, h->L[C2B].cout, w, b);

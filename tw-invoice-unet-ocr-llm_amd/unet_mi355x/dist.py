@@ -24,32 +24,53 @@ def shard_bounds(n_total: int, rank: int, world: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def all_gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
-    """Gather the per-rank shards (dim 0, sizes per shard_bounds) into the full batch.
+class MaskGather:
+    """The one exchange step with its buffers allocated once: every rank writes its shard into
+    ``local`` (the first hi - lo rows of a send buffer padded to the largest shard, padding rows
+    zero), and ``__call__`` all-gathers the send buffers into ``out`` ([world x cap] rows, rank r's
+    shard at rows [r cap, r cap + its size)).  ``rows()`` drops the padding (a copy, outside any
+    timed step).  With "nccl" the collective is RCCL over xGMI; with gloo the same call on CPU."""
 
-    Shards are padded to the largest shard so one all_gather_into_tensor covers ragged
-    batches; the padding is dropped on return.  Order = rank order = original batch order.
-    """
+    def __init__(self, n_total: int, row_shape, dtype, device, group=None, rank=None, world=None):
+        self.group = group
+        self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
+        self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
+        self.n_total = n_total
+        lo, hi = shard_bounds(n_total, self.rank, self.world)
+        self.cap = shard_bounds(n_total, 0, self.world)[1]          # largest shard (rank 0)
+        self.send = torch.zeros((self.cap,) + tuple(row_shape), dtype=dtype, device=device)
+        self.local = self.send[:hi - lo]
+        self.out = self.send if self.world == 1 else \
+            torch.empty((self.world * self.cap,) + tuple(row_shape), dtype=dtype, device=device)
+
+    def __call__(self) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.out, self.send, group=self.group)
+        return self.out
+
+    def rows(self) -> torch.Tensor:
+        """The gathered shards in global batch order without the padding rows."""
+        if self.n_total % self.world == 0:
+            return self.out
+        keep = []
+        for r in range(self.world):
+            a, b = shard_bounds(self.n_total, r, self.world)
+            keep.append(self.out[r * self.cap: r * self.cap + (b - a)])
+        return torch.cat(keep, 0)
+
+
+def all_gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
+    """Gather the per-rank shards (dim 0, sizes per shard_bounds) into the full batch, in rank
+    order = original batch order (one-shot form of MaskGather: allocates its buffers per call)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     lo, hi = shard_bounds(n_total, rank, world)
     if local.shape[0] != hi - lo:
         raise ValueError(f"rank {rank}: local shard has {local.shape[0]} rows, expected {hi - lo}")
-    cap = shard_bounds(n_total, 0, world)[1]          # largest shard (rank 0)
-    if local.shape[0] < cap:
-        pad = torch.zeros((cap - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-        send = torch.cat([local, pad], 0)
-    else:
-        send = local.contiguous()
-    out = torch.empty((world * cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, send, group=group)   # RCCL over xGMI with "nccl"; gloo on CPU
-    if n_total % world == 0:
-        return out
-    keep = []
-    for r in range(world):
-        a, b = shard_bounds(n_total, r, world)
-        keep.append(out[r * cap: r * cap + (b - a)])
-    return torch.cat(keep, 0)
+    g = MaskGather(n_total, tuple(local.shape[1:]), local.dtype, local.device, group, rank, world)
+    g.local.copy_(local)
+    g()
+    return g.rows()
 
 
 class ShardedSegmenter:
@@ -104,9 +125,9 @@ def timed_steps(step, steps: int, warmup: int, sync=None, device=None, group=Non
     return elapsed, [b - a for a, b in zip(marks, marks[1:])]
 
 
-def sharded_mask_step(segment_fn, x_local: torch.Tensor, masks_local: torch.Tensor, n_total: int, group=None):
-    """One data-parallel step of bench.py at N > 1: this rank's forward of its shard into its
-    (bit-packed) mask buffer, then the one exchange step -- the all-gather of every rank's masks.
-    Returns the gathered masks [n_total, ...] in global batch order."""
-    segment_fn(x_local, masks_local)
-    return all_gather_rows(masks_local, n_total, group)
+def sharded_mask_step(segment_fn, x_local: torch.Tensor, gather: MaskGather):
+    """One data-parallel step of bench.py at N > 1: this rank's forward of its shard into its slot of
+    the preallocated send buffer (``gather.local``, bit-packed masks), then the one exchange step --
+    the all-gather of every rank's masks into ``gather.out``.  Allocates nothing."""
+    segment_fn(x_local, gather.local)
+    return gather()

@@ -16,10 +16,26 @@ import threading
 
 import torch
 import torch.nn as nn
+import torch.nn.modules.module as _mm
 
 from . import native
 
 DEFAULT_DTYPE = os.environ.get("UNET_MI355X_DTYPE", "fp32")
+
+# Bumped whenever any module anywhere registers a parameter, buffer or sub-module, or a UNet /
+# DoubleConv converts its tensors (_apply: .to / .cuda / .half): the cached list of tensors whose
+# (data_ptr, _version) signature decides re-packing is then rebuilt.  Between such events the
+# per-forward check reads 136 cached tensors instead of rebuilding state_dict().
+_TREE_EPOCH = [0]
+
+
+def _bump_epoch(*_args):
+    _TREE_EPOCH[0] += 1   # returns None: the hooks never replace what is registered
+
+
+_mm.register_module_parameter_registration_hook(_bump_epoch)
+_mm.register_module_buffer_registration_hook(_bump_epoch)
+_mm.register_module_module_registration_hook(_bump_epoch)
 
 
 class DoubleConv(nn.Module):
@@ -43,6 +59,11 @@ class DoubleConv(nn.Module):
 
     def forward(self, x):  # pragma: no cover - documented limitation
         raise RuntimeError("unet_mi355x: DoubleConv runs only inside UNet.forward (fused native path)")
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        _bump_epoch()
+        return out
 
 
 class UNet(nn.Module):
@@ -88,10 +109,23 @@ class UNet(nn.Module):
         self._handles: dict[int, native.Handle] = {}
         self._packed_sig: dict[int, tuple] = {}
         self._lock = threading.Lock()
+        self._sig_tensors = None
+        self._sig_epoch = -1
 
     # ------------------------------------------------------------------ native plumbing
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        _bump_epoch()
+        return out
+
     def _signature(self):
-        return tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
+        """(data_ptr, _version) of every state_dict tensor: changes on any in-place update
+        (load_state_dict, optimizer steps, ``with no_grad(): p.add_``), on .to() / .data
+        replacement and on re-registration (the cached tensor list is rebuilt then)."""
+        if self._sig_epoch != _TREE_EPOCH[0] or self._sig_tensors is None:
+            self._sig_tensors = list(self.state_dict(keep_vars=True).values())
+            self._sig_epoch = _TREE_EPOCH[0]
+        return tuple((t.data_ptr(), t._version) for t in self._sig_tensors)
 
     def native_handle(self, device: torch.device) -> native.Handle:
         """The packed native handle for ``device`` (re-packs if any parameter changed)."""
@@ -120,7 +154,8 @@ class UNet(nn.Module):
             # the reference fails inside torch.cat for such sizes
             raise RuntimeError(f"UNet input H and W must be divisible by 16, got {tuple(x.shape[2:])}")
 
-    def _run(self, x: torch.Tensor, want_logits: bool, mask_kind: int, want_boxes: bool = False):
+    def _run(self, x: torch.Tensor, want_logits: bool, mask_kind: int, want_boxes: bool = False,
+             out_masks: torch.Tensor | None = None, out_boxes: torch.Tensor | None = None):
         self._check_input(x)
         if self.training and torch.is_grad_enabled():
             raise RuntimeError("unet_mi355x.UNet is inference-only (eval BatchNorm folded, no autograd); "
@@ -133,16 +168,22 @@ class UNet(nn.Module):
         logits = masks = None
         if want_logits:
             logits = torch.empty((n, self.n_classes, hh, ww), device=x.device, dtype=torch.float32)
-        if mask_kind == native.MASK_U8:
-            masks = torch.empty((n, self.n_classes, hh, ww), device=x.device, dtype=torch.uint8)
-        elif mask_kind == native.MASK_BITS:
-            masks = torch.empty((n, self.n_classes, hh, ww // 8), device=x.device, dtype=torch.uint8)
+        if mask_kind != native.MASK_NONE:
+            shape = (n, self.n_classes, hh, ww if mask_kind == native.MASK_U8 else ww // 8)
+            if out_masks is not None:   # a caller-owned buffer reused across calls (run_unet)
+                if (out_masks.dtype != torch.uint8 or tuple(out_masks.shape) != shape or
+                        not out_masks.is_contiguous() or out_masks.device != x.device):
+                    raise ValueError(f"out masks must be a contiguous uint8 {shape} tensor on {x.device}")
+                masks = out_masks
+            else:
+                masks = torch.empty(shape, device=x.device, dtype=torch.uint8)
         stream = torch.cuda.current_stream(x.device).cuda_stream
         boxes = None
         h.reserve(n, hh, ww)   # grows the workspace if needed (a no-op otherwise); forwards never allocate
         with torch.cuda.device(x.device):
             if want_boxes:
-                boxes = torch.empty((n, self.n_classes, 4), device=x.device, dtype=torch.int32)
+                boxes = out_boxes if out_boxes is not None else \
+                    torch.empty((n, self.n_classes, 4), device=x.device, dtype=torch.int32)
                 h.forward_boxes(x, logits, masks, mask_kind, boxes, stream)
             else:
                 h.forward(x, logits, masks, mask_kind, stream)
@@ -165,15 +206,17 @@ class UNet(nn.Module):
         logits, masks = self._run(x, with_logits, native.MASK_BITS if packed else native.MASK_U8)
         return (masks, logits) if with_logits else masks
 
-    def forward_boxes(self, x: torch.Tensor, masks: str | None = None):
+    def forward_boxes(self, x: torch.Tensor, masks: str | None = None, out=None):
         """Fused masks + per-(image, field) bounding boxes on the device (inference.py:72-90).
 
         Returns int32 boxes [N, n_classes, 4] = (x_min, y_min, x_max, y_max) in mask pixels,
         inclusive, (-1, -1, -1, -1) for an empty mask -- the np.where -> min/max of run_unet.
         ``masks`` = None (boxes only), "u8" or "bits": also return that mask tensor first.
+        ``out`` = (masks tensor or None, boxes tensor): caller-owned device buffers to fill.
         """
         kind = {None: native.MASK_NONE, "u8": native.MASK_U8, "bits": native.MASK_BITS}[masks]
-        _, m, boxes = self._run(x, False, kind, want_boxes=True)
+        om, ob = out if out is not None else (None, None)
+        _, m, boxes = self._run(x, False, kind, want_boxes=True, out_masks=om, out_boxes=ob)
         return boxes if masks is None else (m, boxes)
 
     def preprocess(self, img: torch.Tensor, size: int = 512, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -24,6 +24,7 @@ DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16
 MASK_NONE, MASK_U8, MASK_BITS = 0, 1, 2
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
 COMM_ID_BYTES = 128
+ABI_VERSION = 2   # include/unet_mi355x.h UNET_ABI_VERSION
 IN_F32, IN_U8 = 0, 1
 
 # every function include/unet_mi355x.h declares: name -> (restype, argtypes)
@@ -85,7 +86,7 @@ def load_library(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.unet_abi_version() != 1:
+        if lib.unet_abi_version() != ABI_VERSION:
             raise RuntimeError("unet_mi355x: ABI version mismatch")
         _lib = lib
         return lib
@@ -235,18 +236,27 @@ class Handle:
         buf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
         with self.lock:
             check(self.lib.unet_comm_init(self._h, rank, nranks, buf), "unet_comm_init")
+        self.nranks = nranks
 
     def allgather(self, send: torch.Tensor, recv: torch.Tensor, stream: int) -> None:
         """recv[r] = rank r's ``send`` (contiguous device tensors, recv = nranks x send bytes)."""
         if not (send.is_contiguous() and recv.is_contiguous()):
             raise ValueError("send and recv must be contiguous")
+        nranks = getattr(self, "nranks", None)
+        if nranks is None:
+            raise RuntimeError("unet_allgather: no communicator, call comm_init first")
+        sb = send.numel() * send.element_size()
+        if recv.numel() * recv.element_size() != nranks * sb:   # RCCL would write past a short recv
+            raise ValueError(f"recv holds {recv.numel() * recv.element_size()} bytes, expected nranks x send = "
+                             f"{nranks} x {sb}")
         with self.lock:
             check(self.lib.unet_allgather(self._h, send.data_ptr(), recv.data_ptr(),
-                                          send.numel() * send.element_size(), stream), "unet_allgather")
+                                          sb, stream), "unet_allgather")
 
     def comm_destroy(self) -> None:
         with self.lock:
             check(self.lib.unet_comm_destroy(self._h), "unet_comm_destroy")
+        self.nranks = None
 
     def launch_labels(self) -> list:
         """Kernel instantiation of every launch of a forward (include/unet_mi355x.h order)."""
