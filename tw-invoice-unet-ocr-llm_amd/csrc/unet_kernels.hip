@@ -1490,6 +1490,12 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     for (int i = tid; i < a.ncls * 64; i += 64 * NW) headw_s[i] = a.head_w[i];
     if (tid < a.ncls) headb_s[tid] = a.head_b[tid];
   }
+  // EPI_UPFUSE: the ConvTranspose bias (4 quadrants x 64 rows) in the head's LDS space.  Read
+  // from global inside the quadrant loop it cost a vmcnt wait there -- in-order, so a drain of
+  // every DMA in flight and of the previous quadrants' scatter stores, four times per tile.
+  static_assert(kMaxClasses * 64 >= 4 * 64, "up1 bias in the head parameter space");
+  if (UPF)
+    for (int i = tid; i < 4 * 64; i += 64 * NW) headw_s[i] = a.bias2[i];
   if constexpr (WST) {
     wait_vm_barrier<0>();
   } else {
@@ -1706,7 +1712,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         else wait_vm_barrier_rt(young * wcnt);   // the last halo issue is older than W(g+1)
         // no vmcnt(0) drain: the stores retire under the next step's wait (see ring_body)
         conv_epilogue<TO, TO, TP, EPI_UPSCATTER, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[0]), n, ty * 16,
-                                                     tx * TW, wp * TP, 64 * quad, a.bias2 + 64 * quad, nullptr,
+                                                     tx * TW, wp * TP, 64 * quad, headw_s + 64 * quad, nullptr,
                                                      nullptr, a.out2, a.ldo2, a.Cout / 2);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -1780,8 +1786,11 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
   constexpr int BI = 256 / (16 * NW);         // B DMA instructions per wave and step
   constexpr int ASLOT = BR * 64, BSLOT = 256 * 64, SLOT = ASLOT + BSLOT;
   static_assert((NS == 3 || NS == 4) && TC % 4 == 0, "ring depth / row tile");
-  static_assert(NS * SLOT <= 160 * 1024 / (WRW == 1 ? 2 : 1), "blocks per CU");
-  __shared__ __attribute__((aligned(16))) char lds[NS * SLOT];   // the epilogue reads the bias from global (L2)
+  static_assert(NS * SLOT + BR * 4 <= 160 * 1024 / (WRW == 1 ? 2 : 1), "blocks per CU");
+  __shared__ __attribute__((aligned(16))) char lds[NS * SLOT];
+  // the walker's row-tile bias, for the epilogue: read from global there, its vmcnt wait (in
+  // order) drained every DMA in flight and the previous pixel groups' scatter stores per tile
+  __shared__ __attribute__((aligned(16))) float bias_s[BR];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave >> 2, wp = wave & 3;   // row group (WRW = 2), pixel group
@@ -1850,6 +1859,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
 #pragma unroll
   for (int k = 0; k < NS - 1; ++k)
     if (k < total) issue(k);
+  for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];   // (the wait below covers it)
   {   // step 0 landed; steps 1 .. NS-2 may stay in flight
     const int young = total - 1 < NS - 2 ? total - 1 : NS - 2;
     if (young == 2) wait_vm_barrier<2 * (WI + BI)>(); else if (young == 1) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
@@ -1897,7 +1907,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
       for (int h = 0; h < TC / 4; ++h)
         conv_epilogue<TO, TO, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
                                             tx * 16, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
-                                            a.bias + ct * BR + wr * 16 * TC + 64 * h, nullptr,
+                                            bias_s + wr * 16 * TC + 64 * h, nullptr,
                                             nullptr);
 #pragma unroll
       for (int t = 0; t < TC; ++t)
