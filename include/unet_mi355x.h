@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 2   /* 2: unet_forward requires unet_reserve; Cfg renumbered; fp16 range check */
+#define UNET_ABI_VERSION 3   /* 2: unet_forward requires unet_reserve; Cfg renumbered; fp16 range check. 3: unet_crop_stats */
 
 /* error codes */
 #define UNET_OK 0
@@ -136,6 +136,19 @@ int unet_forward_boxes(unet_handle* h, const void* x, int x_layout, int x_dtype,
  * uploads them synchronously).  Stream-ordered on hip_stream. */
 int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channels,
                     float* x, int oh, int ow, void* hip_stream);
+
+/* The crop step of run_unet (inference.py:92-127) on the device photo, so the host never reads
+ * crop pixels: for every mask box (unet_forward_boxes' output, in a box_h x box_w mask), the crop
+ * rectangle in photo pixels -- the reference's float64 arithmetic: scale = iw / box_w, x1 =
+ * int(x_min * scale), x2 = int(x_max * scale), pad_x = int((x2 - x1) * pad) (pad = 0.15), clamp
+ * to [0, iw] (y likewise) -- and the sum of the crop's uint8 values over every channel.  The
+ * reference's rejections are then host tests: x2 <= x1 or y2 <= y1 (empty crop), and
+ * np.array(crop).mean() < 3  <=>  sum < 3 * (x2 - x1) * (y2 - y1) * channels (numpy's float64 sum
+ * of the integers is exact).  img: device uint8 HWC [ih][iw][channels] (unet_preprocess's input);
+ * boxes: device int32 [n_boxes][4]; rects: device int32 [n_boxes][4] (x1, y1, x2, y2; -1s for an
+ * empty box); sums: device uint64 [n_boxes].  Needs no handle; stream-ordered on hip_stream. */
+int unet_crop_stats(const void* img, int ih, int iw, int channels, const int32_t* boxes, int n_boxes,
+                    int box_h, int box_w, double pad, int32_t* rects, uint64_t* sums, void* hip_stream);
 
 /* Number of launch slots in one forward (first conv, 17 implicit-GEMM 3x3 convs with
  * the fused pool / head epilogues, 4 ConvTranspose2d), in execution order:

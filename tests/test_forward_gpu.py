@@ -755,7 +755,7 @@ def test_run_unet_boundary_matches_reference_golden():
         # the crop rules (inference.py:92-127) applied to the box of the REFERENCE's mask reproduce
         # its crop byte for byte; our own crop must too whenever our mask has the same box (a mask
         # pixel off inside the box changes nothing downstream)
-        ref_box = inf.mask_box(ref)
+        ref_box = _np_box(ref)
         from_ref = inf.crop_from_box(pil, ref_box)
         if bool(z["crop_none_" + k]):
             assert crops[k] is None and from_ref is None
@@ -764,10 +764,53 @@ def test_run_unet_boundary_matches_reference_golden():
         assert hashlib.sha256(np.asarray(from_ref).tobytes()).hexdigest() == want
         arr = np.asarray(crops[k])
         assert list(arr.shape) == list(z["crop_shape_" + k])
-        if inf.mask_box(masks[k]) == ref_box:
+        if _np_box(masks[k]) == ref_box:
             assert hashlib.sha256(arr.tobytes()).hexdigest() == want, k
         else:
-            print(f"run_unet {k}: box {inf.mask_box(masks[k])} vs reference {ref_box}")
+            print(f"run_unet {k}: box {_np_box(masks[k])} vs reference {ref_box}")
+
+
+def _np_box(mask):
+    """inference.py:84-90: np.where -> (x_min, y_min, x_max, y_max), None for an empty mask."""
+    ys, xs = np.where(mask)
+    return None if len(xs) == 0 else (int(xs.min()), int(ys.min()), int(xs.max()), int(ys.max()))
+
+
+@pytest.mark.parametrize("h,w,c", [(400, 600, 3), (700, 300, 1), (3024, 4032, 3), (23, 37, 3)])
+def test_crop_stats_match_host_crop_rules(h, w, c):
+    """unet_crop_stats (device) == the reference's crop arithmetic (inference.py:92-127, restated
+    by inference.crop_rect) and numpy's crop pixel sums, for empty / 1-pixel / border / whole-mask /
+    random boxes; and crop_from_stats on them == crop_from_box (incl. the near-black rejection, on
+    a dark photo whose crop means straddle 3)."""
+    from PIL import Image
+    from unet_mi355x import inference as inf, native
+    rng = np.random.default_rng(h * 7 + w)
+    for dark in (False, True):
+        arr = rng.integers(0, 7 if dark else 256, (h, w, c) if c == 3 else (h, w), dtype=np.uint8)
+        pil = Image.fromarray(arr)
+        boxes = [(-1, -1, -1, -1), (0, 0, 0, 0), (511, 511, 511, 511), (0, 0, 511, 511), (3, 500, 9, 511)]
+        for _ in range(59):
+            x0, y0 = rng.integers(0, 512, 2)
+            boxes.append((x0, y0, min(511, x0 + rng.integers(0, 200)), min(511, y0 + rng.integers(0, 200))))
+        b = torch.tensor(np.array(boxes, dtype=np.int32)).to(DEV)
+        rects = torch.empty((len(boxes), 4), dtype=torch.int32, device=DEV)
+        sums = torch.empty((len(boxes),), dtype=torch.int64, device=DEV)
+        img = torch.from_numpy(arr.reshape(h, w, c)).to(DEV)
+        native.crop_stats(img, b, 512, 512, inf.CROP_PAD, rects, sums, torch.cuda.current_stream().cuda_stream)
+        rects, sums = rects.cpu().numpy(), sums.cpu().numpy()
+        for i, box in enumerate(boxes):
+            if box[2] < 0:
+                assert tuple(rects[i]) == (-1, -1, -1, -1)
+                want = None
+            else:
+                r = inf.crop_rect(box, w, h)
+                assert tuple(int(v) for v in rects[i]) == r, (box, rects[i], r)
+                assert int(sums[i]) == int(arr[r[1]:r[3], r[0]:r[2]].astype(np.int64).sum()), box
+                want = inf.crop_from_box(pil, box)
+            got = inf.crop_from_stats(pil, rects[i], sums[i], c)
+            assert (got is None) == (want is None), (box, dark)
+            if got is not None:
+                assert np.array_equal(np.asarray(got), np.asarray(want))
 
 
 def test_run_unet_batch_equals_per_photo_calls():

@@ -57,14 +57,32 @@ def _np_box(mask):
     return None if len(xs) == 0 else (xs.min(), ys.min(), xs.max(), ys.max())
 
 
-def test_crops_from_boxes_equal_crops_from_masks():
-    """run_unet's crop step from device boxes (x0, y0, x1, y1 / -1s) == the reference's
-    np.where path (inference.py:84-127) on the same masks, incl. empty / 1-pixel masks."""
+def _reference_crops(pil, masks):
+    """inference.py:84-127 through the oracle's restatement (oracle.crop_boxes + near-black rule)."""
+    from oracle import unet_oracle as orc
+    out = {}
+    for k, box in orc.crop_boxes(masks, *pil.size).items():
+        crop = None if box is None else pil.crop(box)
+        if crop is not None:
+            arr = np.array(crop)
+            if arr.size == 0 or arr.mean() < 3:
+                crop = None
+        out[k] = crop
+    return out
+
+
+def test_crops_from_boxes_and_stats_equal_reference_crops():
+    """run_unet's crop step -- from device boxes (crop_from_box), and from device crop statistics
+    (crop_from_stats: rectangle + pixel sum, the near-black test as sum < 3 * count) -- equals the
+    reference's np.where path (inference.py:84-127) on the same masks: empty / 1-pixel masks,
+    random and dim photos (crop means around 3), RGB and L."""
     from PIL import Image
     from unet_mi355x import inference as inf
     rng = np.random.default_rng(0)
-    img = Image.fromarray(rng.integers(0, 256, (400, 600, 3), dtype=np.uint8), mode="RGB")
-    dark = Image.fromarray(np.zeros((300, 200, 3), dtype=np.uint8), mode="RGB")
+    photos = [Image.fromarray(rng.integers(0, 256, (400, 600, 3), dtype=np.uint8), mode="RGB"),
+              Image.fromarray(np.zeros((300, 200, 3), dtype=np.uint8), mode="RGB"),
+              Image.fromarray(rng.integers(0, 7, (333, 517, 3), dtype=np.uint8), mode="RGB"),
+              Image.fromarray(rng.integers(0, 7, (500, 280), dtype=np.uint8), mode="L")]
     for trial in range(20):
         masks = {}
         for i, k in enumerate(inf.FIELDS):
@@ -77,10 +95,18 @@ def test_crops_from_boxes_equal_crops_from_masks():
                 m[y0:y0 + rng.integers(1, 100), x0:x0 + rng.integers(1, 100)] = rng.random() < 0.9
             masks[k] = m
         boxes = np.array([_np_box(masks[k]) or (-1, -1, -1, -1) for k in inf.FIELDS], dtype=np.int32)
-        for pil in (img, dark):
-            a = inf.masks_to_crops(pil, masks)
+        for pil in photos:
+            a = _reference_crops(pil, masks)
             b = inf.boxes_to_crops(pil, boxes)
+            arr = np.asarray(pil)
+            ch = 3 if arr.ndim == 3 else 1
+            c = {}
+            for i, k in enumerate(inf.FIELDS):
+                r = (-1, -1, -1, -1) if boxes[i, 2] < 0 else inf.crop_rect(boxes[i], *pil.size)
+                s = 0 if r[2] < 0 else int(arr[r[1]:r[3], r[0]:r[2]].astype(np.int64).sum())
+                c[k] = inf.crop_from_stats(pil, r, s, ch)
             for k in inf.FIELDS:
-                assert (a[k] is None) == (b[k] is None), (trial, k)
+                assert (a[k] is None) == (b[k] is None) == (c[k] is None), (trial, k, pil.mode)
                 if a[k] is not None:
                     assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]))
+                    assert np.array_equal(np.asarray(a[k]), np.asarray(c[k]))

@@ -1072,6 +1072,20 @@ int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channel
   return UNET_OK;
 }
 
+int unet_crop_stats(const void* img, int ih, int iw, int channels, const int32_t* boxes, int n_boxes, int box_h,
+                    int box_w, double pad, int32_t* rects, uint64_t* sums, void* stream) {
+  if (!img || !boxes || !rects || !sums) return fail(UNET_EINVAL, "null argument");
+  if (channels != 1 && channels != 3) return fail(UNET_EINVAL, "channels must be 1 (L) or 3 (RGB)");
+  if (ih <= 0 || iw <= 0 || (long long)ih * iw > (1LL << 30) || box_h <= 0 || box_w <= 0 || n_boxes <= 0 ||
+      n_boxes > 65535 || !(pad >= 0.0 && pad < 1.0))
+    return fail(UNET_EINVAL, "bad image size, box geometry, box count or pad");
+  hipError_t e = launch_crop_stats(static_cast<const uint8_t*>(img), ih, iw, channels, boxes, n_boxes, box_h, box_w,
+                                   pad, rects, reinterpret_cast<unsigned long long*>(sums),
+                                   static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail(UNET_EHIP, std::string("crop stats launch: ") + hipGetErrorString(e));
+  return UNET_OK;
+}
+
 int unet_num_launches(void) { return UNET_NUM_LAUNCHES; }
 
 const char* unet_launch_label(const unet_handle* h, int i) {

@@ -146,5 +146,8 @@ hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int C, uin
 constexpr int kMaxBoxW = 16384;
 hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, int H, int W, int* boxes,
                              hipStream_t s);
+// crop rectangles + crop pixel sums of mask boxes on the device photo (unet_preprocess.hip)
+hipError_t launch_crop_stats(const uint8_t* img, int ih, int iw, int C, const int* boxes, int n_boxes, int bh, int bw,
+                             double pad, int* rects, unsigned long long* sums, hipStream_t s);
 
 }  // namespace unet

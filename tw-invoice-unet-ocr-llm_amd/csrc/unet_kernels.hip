@@ -2247,11 +2247,22 @@ hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------------
 // per-(image, field) bounding box of a mask: inference.py:84-90 (np.where(mask) ->
 // xs.min(), xs.max(), ys.min(), ys.max()) on the GPU, 4 ints instead of H*W host bytes.
-// One block per (n, c).  Bit-packed masks are read as little-endian 16-bit words (bit j of
-// word w = pixel 16*w + j; W % 16 == 0); each thread ORs its words into a per-block column
-// mask in LDS and keeps the first / last row with a set bit.  Empty mask -> (-1,-1,-1,-1).
+// One block per (n, c).  The mask is walked as 16-pixel column words (bit j of word w = pixel
+// 16*w + j: a little-endian 16-bit word of a bit-packed mask, or 16 bytes of a uint8 mask
+// reduced to their nonzero bits); thread t takes words t, t + 256, ..., so with W / 16 dividing
+// 256 it always sees the same column word and ORs it in a register (one LDS atomic per thread
+// instead of one per set pixel), and keeps the first / last row with a set bit.  Four loads are
+// in flight per thread.  Empty mask -> (-1,-1,-1,-1).
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void mask_boxes_kernel(const uint8_t* __restrict__ masks, int kind, int H, int W,
+__device__ __forceinline__ unsigned nz_bits4(unsigned d) {   // bit j = byte j of d nonzero
+  d |= d >> 4;
+  d |= d >> 2;
+  d |= d >> 1;
+  return (d & 1u) | ((d >> 7) & 2u) | ((d >> 14) & 4u) | ((d >> 21) & 8u);
+}
+
+template <int KIND, bool VEC>
+__global__ __launch_bounds__(256) void mask_boxes_kernel(const uint8_t* __restrict__ masks, int H, int W,
                                                         int* __restrict__ boxes) {
   __shared__ unsigned col_or[kMaxBoxW / 16];
   __shared__ int ymin_s, ymax_s, xmin_s, xmax_s;
@@ -2260,31 +2271,45 @@ __global__ __launch_bounds__(256) void mask_boxes_kernel(const uint8_t* __restri
   for (int i = tid; i < words; i += 256) col_or[i] = 0u;
   if (tid == 0) { ymin_s = 0x7FFFFFFF; ymax_s = -1; xmin_s = 0x7FFFFFFF; xmax_s = -1; }
   __syncthreads();
-  int ymin = 0x7FFFFFFF, ymax = -1;
-  if (kind == MASK_BITS) {
-    const uint16_t* m = reinterpret_cast<const uint16_t*>(masks) + (size_t)blockIdx.x * H * words;
-    const int total = H * words;
-    for (int i = tid; i < total; i += 256) {
-      const unsigned v = m[i];
-      if (v) {
-        const int y = i / words;
-        ymin = min(ymin, y);
-        ymax = max(ymax, y);
-        atomicOr(&col_or[i - y * words], v);
-      }
+  const int total = H * words;
+  const size_t plane = KIND == MASK_BITS ? (size_t)H * (W / 8) : (size_t)H * W;
+  const uint8_t* base = masks + (size_t)blockIdx.x * plane;
+  auto word_at = [&](int i) -> unsigned {   // 16-pixel column word i of the plane
+    if constexpr (KIND == MASK_BITS) {
+      return reinterpret_cast<const uint16_t*>(base)[i];
+    } else if constexpr (VEC) {
+      const uint4 v = reinterpret_cast<const uint4*>(base)[i];
+      return nz_bits4(v.x) | (nz_bits4(v.y) << 4) | (nz_bits4(v.z) << 8) | (nz_bits4(v.w) << 12);
+    } else {
+      unsigned b = 0;
+      for (int j = 0; j < 16; ++j) b |= (base[16 * i + j] ? 1u : 0u) << j;
+      return b;
     }
-  } else {
-    const uint8_t* m = masks + (size_t)blockIdx.x * H * W;
-    const int total = H * W;
-    for (int i = tid; i < total; i += 256) {
-      if (m[i]) {
-        const int y = i / W, x = i - y * W;
+  };
+  int ymin = 0x7FFFFFFF, ymax = -1, cw = -1;
+  unsigned cacc = 0;
+  for (int i0 = tid; i0 < total; i0 += 4 * 256) {
+    unsigned v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = i0 + k * 256 < total ? word_at(i0 + k * 256) : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = i0 + k * 256;
+      if (i >= total) break;
+      const int y = i / words, w = i - y * words;
+      if (w != cw) {
+        if (cacc) atomicOr(&col_or[cw], cacc);
+        cacc = 0;
+        cw = w;
+      }
+      if (v[k]) {
         ymin = min(ymin, y);
         ymax = max(ymax, y);
-        atomicOr(&col_or[x >> 4], 1u << (x & 15));
+        cacc |= v[k];
       }
     }
   }
+  if (cacc) atomicOr(&col_or[cw], cacc);
   if (ymax >= 0) { atomicMin(&ymin_s, ymin); atomicMax(&ymax_s, ymax); }
   __syncthreads();
   for (int i = tid; i < words; i += 256) {
@@ -2308,7 +2333,14 @@ __global__ __launch_bounds__(256) void mask_boxes_kernel(const uint8_t* __restri
 hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, int H, int W, int* boxes,
                              hipStream_t s) {
   if (W % 16 || W > kMaxBoxW || (kind != MASK_BITS && kind != MASK_U8)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(mask_boxes_kernel, dim3((unsigned)(N * ncls)), dim3(256), 0, s, masks, kind, H, W, boxes);
+  const dim3 grid((unsigned)(N * ncls)), block(256);
+  if (kind == MASK_BITS) {
+    hipLaunchKernelGGL((mask_boxes_kernel<MASK_BITS, false>), grid, block, 0, s, masks, H, W, boxes);
+  } else if (reinterpret_cast<uintptr_t>(masks) % 16 == 0) {
+    hipLaunchKernelGGL((mask_boxes_kernel<MASK_U8, true>), grid, block, 0, s, masks, H, W, boxes);
+  } else {
+    hipLaunchKernelGGL((mask_boxes_kernel<MASK_U8, false>), grid, block, 0, s, masks, H, W, boxes);
+  }
   return hipGetLastError();
 }
 

@@ -12,6 +12,8 @@
 // itself checked against Pillow (tests/test_preprocess_cpu.py).
 #include "unet_internal.h"
 
+#include <algorithm>
+
 namespace unet {
 
 namespace {
@@ -93,6 +95,71 @@ hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int C, uin
                        p.ow, out);
   else
     hipLaunchKernelGGL(to_planar_f32_kernel, grid, dim3(256), 0, s, src, stride, C, p.oh, p.ow, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// Crop statistics (inference.py:92-127) on the device photo: per (image, field) mask box, the
+// crop rectangle in photo pixels and the sum of the crop's uint8 values, so the host applies the
+// reference's rejection rules without reading pixels.  The rectangle arithmetic is the
+// reference's, in float64 as Python evaluates it: scale = ow / IMG_SIZE (true division),
+// x1 = int(mx1 * scale) (truncation), pad = int((x2 - x1) * 0.15), clamp to [0, ow] / [0, oh].
+// "arr.mean() < 3" over the crop's uint8 values (numpy's float64 pairwise sum of integers is
+// exact below 2^53) is "sum < 3 * count" -- the host tests that.  Grid (row blocks, boxes); each
+// block sums its rows (64-bit, one atomic per wave) into sums[box], zeroed by the launcher.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void crop_rect(const int* b, int ih, int iw, int bh, int bw, double pad, int& x1, int& y1,
+                                          int& x2, int& y2) {
+  const double sx = (double)iw / (double)bw, sy = (double)ih / (double)bh;
+  x1 = (int)((double)b[0] * sx);
+  x2 = (int)((double)b[2] * sx);
+  y1 = (int)((double)b[1] * sy);
+  y2 = (int)((double)b[3] * sy);
+  const int px = (int)((double)(x2 - x1) * pad), py = (int)((double)(y2 - y1) * pad);
+  x1 = max(0, x1 - px);
+  y1 = max(0, y1 - py);
+  x2 = min(iw, x2 + px);
+  y2 = min(ih, y2 + py);
+}
+
+__global__ __launch_bounds__(256) void crop_stats_kernel(const uint8_t* __restrict__ img, int ih, int iw, int C,
+                                                        const int* __restrict__ boxes, int bh, int bw, double pad,
+                                                        int* __restrict__ rects,
+                                                        unsigned long long* __restrict__ sums) {
+  const int i = blockIdx.y;
+  const int* b = boxes + 4 * i;
+  if (b[2] < 0) {   // empty mask
+    if (blockIdx.x == 0 && threadIdx.x < 4) rects[4 * i + threadIdx.x] = -1;
+    return;
+  }
+  int x1, y1, x2, y2;
+  crop_rect(b, ih, iw, bh, bw, pad, x1, y1, x2, y2);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    rects[4 * i] = x1;
+    rects[4 * i + 1] = y1;
+    rects[4 * i + 2] = x2;
+    rects[4 * i + 3] = y2;
+  }
+  if (x2 <= x1 || y2 <= y1) return;
+  const int rowlen = (x2 - x1) * C;
+  unsigned long long acc = 0;
+  for (int y = y1 + (int)blockIdx.x; y < y2; y += (int)gridDim.x) {
+    const uint8_t* row = img + ((size_t)y * iw + x1) * C;
+    for (int k = threadIdx.x; k < rowlen; k += 256) acc += row[k];
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(sums + i, acc);
+}
+
+hipError_t launch_crop_stats(const uint8_t* img, int ih, int iw, int C, const int* boxes, int n_boxes, int bh, int bw,
+                             double pad, int* rects, unsigned long long* sums, hipStream_t s) {
+  if ((C != 1 && C != 3) || ih <= 0 || iw <= 0 || bh <= 0 || bw <= 0 || n_boxes <= 0) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(sums, 0, (size_t)n_boxes * sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  const int rows_per = 8;
+  const unsigned gx = (unsigned)std::min(64, (ih + rows_per - 1) / rows_per);
+  hipLaunchKernelGGL(crop_stats_kernel, dim3(gx, (unsigned)n_boxes), dim3(256), 0, s, img, ih, iw, C, boxes, bh, bw,
+                     pad, rects, sums);
   return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 from PIL import Image
 
+from . import native
 from .model import UNet
 
 DEVICE = "cuda" if torch.cuda.is_available() else "cpu"   # inference.py:9
@@ -67,20 +68,25 @@ def preprocess(pil_img: Image.Image) -> torch.Tensor:
     return torch.from_numpy(preprocess_array(pil_img)).unsqueeze(0).to(DEVICE)
 
 
+def crop_rect(box, ow: int, oh: int):
+    """inference.py:96-112: mask-space box (x_min, y_min, x_max, y_max) -> crop rectangle in
+    photo pixels (float64 scale, int() truncation, 15 % pad, clamp).  The device twin is
+    unet_crop_stats (csrc/unet_preprocess.hip, crop_rect)."""
+    mx1, my1, mx2, my2 = (int(v) for v in box)
+    scale_x, scale_y = ow / IMG_SIZE, oh / IMG_SIZE
+    x1, x2 = int(mx1 * scale_x), int(mx2 * scale_x)
+    y1, y2 = int(my1 * scale_y), int(my2 * scale_y)
+    pad_x, pad_y = int((x2 - x1) * CROP_PAD), int((y2 - y1) * CROP_PAD)
+    return max(0, x1 - pad_x), max(0, y1 - pad_y), min(ow, x2 + pad_x), min(oh, y2 + pad_y)
+
+
 def crop_from_box(pil_img: Image.Image, box):
     """inference.py:92-127 for one field: mask-space box (x_min, y_min, x_max, y_max), or None
     for an empty mask -> original scale -> 15% pad -> clamp -> crop, rejecting degenerate and
     near-black crops (None)."""
     if box is None:
         return None
-    mx1, my1, mx2, my2 = (int(v) for v in box)
-    ow, oh = pil_img.size
-    scale_x, scale_y = ow / IMG_SIZE, oh / IMG_SIZE
-    x1, x2 = int(mx1 * scale_x), int(mx2 * scale_x)
-    y1, y2 = int(my1 * scale_y), int(my2 * scale_y)
-    pad_x, pad_y = int((x2 - x1) * CROP_PAD), int((y2 - y1) * CROP_PAD)
-    x1, y1 = max(0, x1 - pad_x), max(0, y1 - pad_y)
-    x2, y2 = min(ow, x2 + pad_x), min(oh, y2 + pad_y)
+    x1, y1, x2, y2 = crop_rect(box, *pil_img.size)
     if x2 <= x1 or y2 <= y1:
         return None
     crop = pil_img.crop((x1, y1, x2, y2))
@@ -90,24 +96,22 @@ def crop_from_box(pil_img: Image.Image, box):
     return crop
 
 
+def crop_from_stats(pil_img: Image.Image, rect, pixel_sum: int, channels: int):
+    """crop_from_box from device crop statistics (unet_crop_stats): the rectangle and the sum of
+    the crop's uint8 values.  np.array(crop).mean() < 3 is pixel_sum < 3 * count exactly (numpy
+    sums the integers in float64 without rounding below 2^53), so no crop pixel is read here."""
+    x1, y1, x2, y2 = (int(v) for v in rect)
+    if x2 <= x1 or y2 <= y1:   # also the -1s of an empty mask
+        return None
+    if int(pixel_sum) < 3 * (x2 - x1) * (y2 - y1) * channels:
+        return None
+    return pil_img.crop((x1, y1, x2, y2))
+
+
 def boxes_to_crops(pil_img: Image.Image, boxes) -> dict:
     """Crops from device-computed mask boxes (int32 [n_fields, 4], -1s = empty mask)."""
     b = np.asarray(boxes)
     return {k: crop_from_box(pil_img, None if b[i, 2] < 0 else b[i]) for i, k in enumerate(FIELDS)}
-
-
-def mask_box(mask: np.ndarray):
-    """inference.py:84-90: (x_min, y_min, x_max, y_max) of a mask's pixels, None if empty (the
-    host twin of the device mask_boxes_kernel)."""
-    ys, xs = np.where(mask)
-    if len(xs) == 0:
-        return None
-    return int(xs.min()), int(ys.min()), int(xs.max()), int(ys.max())
-
-
-def masks_to_crops(pil_img: Image.Image, masks: dict) -> dict:
-    """inference.py:84-127 from host masks: bbox per mask, then the crop rules of crop_from_box."""
-    return {k: crop_from_box(pil_img, mask_box(m)) for k, m in masks.items()}
 
 
 class _Staging:
@@ -122,8 +126,12 @@ class _Staging:
         self.x = torch.empty((1, 3, IMG_SIZE, IMG_SIZE), dtype=torch.float32, device=self.device)
         self.m = torch.empty((1, len(FIELDS), IMG_SIZE, IMG_SIZE), dtype=torch.uint8, device=self.device)
         self.b = torch.empty((1, len(FIELDS), 4), dtype=torch.int32, device=self.device)
+        self.r = torch.empty((len(FIELDS), 4), dtype=torch.int32, device=self.device)   # crop rectangles
+        self.s = torch.empty((len(FIELDS),), dtype=torch.int64, device=self.device)     # crop pixel sums
         self.hm = torch.empty(self.m.shape, dtype=torch.uint8).pin_memory()
         self.hb = torch.empty(self.b.shape, dtype=torch.int32).pin_memory()
+        self.hr = torch.empty(self.r.shape, dtype=torch.int32).pin_memory()
+        self.hs = torch.empty(self.s.shape, dtype=torch.int64).pin_memory()
 
     def upload(self, arr: np.ndarray) -> torch.Tensor:
         """uint8 [H, W(, C)] host photo -> device tensor of the same shape (pinned, async)."""
@@ -151,6 +159,7 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
         if st is None:
             st = _staging[str(DEVICE)] = _Staging(DEVICE)
     with st.lock, torch.no_grad():
+        img = None
         if pil_img.mode in ("RGB", "L"):
             # inference.py:63-64 on the GPU: Pillow-exact BICUBIC resize + convert("RGB") + /255
             img = st.upload(np.asarray(pil_img))
@@ -160,13 +169,23 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
             x = preprocess(pil_img.resize((IMG_SIZE, IMG_SIZE)))      # inference.py:63-64
         # fused sigmoid + threshold + per-field bounding boxes on the device
         model.forward_boxes(x, masks="u8", out=(st.m, st.b))
+        stream = torch.cuda.current_stream(st.device)
+        if img is not None:   # crop rectangles + near-black test data from the device photo
+            img3 = img if img.dim() == 3 else img.unsqueeze(-1)
+            native.crop_stats(img3, st.b[0], IMG_SIZE, IMG_SIZE, CROP_PAD, st.r, st.s, stream.cuda_stream)
+            st.hr.copy_(st.r, non_blocking=True)
+            st.hs.copy_(st.s, non_blocking=True)
         st.hm.copy_(st.m, non_blocking=True)
         st.hb.copy_(st.b, non_blocking=True)
-        torch.cuda.current_stream(st.device).synchronize()
+        stream.synchronize()
         m = st.hm.numpy()[0].view(np.bool_).copy()   # the kernel writes 0 / 1 bytes
         boxes = st.hb.numpy()[0].copy()
+        if img is not None:
+            rects, sums, ch = st.hr.numpy().copy(), st.hs.numpy().copy(), (3 if img.dim() == 3 else 1)
     masks = {k: m[i] for i, k in enumerate(FIELDS)}
-    return masks, boxes_to_crops(pil_img, boxes)
+    if img is None:
+        return masks, boxes_to_crops(pil_img, boxes)
+    return masks, {k: crop_from_stats(pil_img, rects[i], sums[i], ch) for i, k in enumerate(FIELDS)}
 
 
 def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = None):
@@ -181,7 +200,7 @@ def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = N
     x = torch.empty((len(pil_imgs), 3, IMG_SIZE, IMG_SIZE), dtype=torch.float32, device=DEVICE)
     for i, pil in enumerate(pil_imgs):
         if pil.mode in ("RGB", "L") and str(DEVICE).startswith("cuda"):
-            img = torch.from_numpy(np.ascontiguousarray(np.asarray(pil))).to(DEVICE)
+            img = torch.from_numpy(np.array(pil)).to(DEVICE)
             model.preprocess(img, IMG_SIZE, out=x[i])
         else:
             x[i] = preprocess(pil.resize((IMG_SIZE, IMG_SIZE)))[0]

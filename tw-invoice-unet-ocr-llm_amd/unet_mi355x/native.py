@@ -24,7 +24,7 @@ DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16
 MASK_NONE, MASK_U8, MASK_BITS = 0, 1, 2
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
 COMM_ID_BYTES = 128
-ABI_VERSION = 2   # include/unet_mi355x.h UNET_ABI_VERSION
+ABI_VERSION = 3   # include/unet_mi355x.h UNET_ABI_VERSION
 IN_F32, IN_U8 = 0, 1
 
 # every function include/unet_mi355x.h declares: name -> (restype, argtypes)
@@ -49,6 +49,7 @@ SIGNATURES = {
     "unet_forward": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp]),
     "unet_forward_boxes": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _i, _vp]),
     "unet_preprocess": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _i, _vp]),
+    "unet_crop_stats": (_i, [_vp, _i, _i, _i, _vp, _i, _i, _i, ctypes.c_double, _vp, _vp, _vp]),
     "unet_num_launches": (_i, []),
     "unet_launch_label": (ctypes.c_char_p, [_vp, _i]),
     "unet_forward_timed": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
@@ -101,6 +102,21 @@ def check(rc: int, what: str):
     if rc == UNET_ENOMEM:
         raise torch.cuda.OutOfMemoryError(msg) if hasattr(torch.cuda, "OutOfMemoryError") else MemoryError(msg)
     raise RuntimeError(msg)
+
+
+def crop_stats(img: torch.Tensor, boxes: torch.Tensor, box_h: int, box_w: int, pad: float,
+               rects: torch.Tensor, sums: torch.Tensor, stream: int) -> None:
+    """unet_crop_stats: crop rectangles (int32 [n, 4]) and crop pixel sums (int64 [n]) of the mask
+    boxes (int32 [n, 4]) on the uint8 HWC device photo ``img``, with run_unet's arithmetic."""
+    if img.dtype != torch.uint8 or img.dim() != 3 or not img.is_contiguous():
+        raise ValueError("img must be a contiguous uint8 [H, W, C] device tensor")
+    n = boxes.numel() // 4
+    for t, dt, shape in ((boxes, torch.int32, (n, 4)), (rects, torch.int32, (n, 4)), (sums, torch.int64, (n,))):
+        if t.dtype != dt or t.numel() != int(np.prod(shape)) or not t.is_contiguous() or t.device != img.device:
+            raise ValueError(f"crop_stats: expected a contiguous {dt} tensor of {shape} on {img.device}")
+    ih, iw, c = img.shape
+    check(load_library().unet_crop_stats(img.data_ptr(), ih, iw, c, boxes.data_ptr(), n, box_h, box_w, float(pad),
+                                         rects.data_ptr(), sums.data_ptr(), stream), "unet_crop_stats")
 
 
 class Handle:
