@@ -37,9 +37,15 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     handles = []
     for c in a.cands:
-        lc, _, uc = c.partition("|")        # "<3x3 layer overrides>|<up overrides>"
+        lc, _, rest = c.partition("|")      # "<3x3 layer overrides>|<up overrides>|K=V;K=V (env)"
+        uc, _, env = rest.partition("|")
         os.environ["UNET_MI355X_CFG"] = lc
         os.environ["UNET_MI355X_UPCFG"] = uc
+        for k in ("UNET_MI355X_PF",):
+            os.environ.pop(k, None)
+        for kv in filter(None, env.split(";")):
+            k, _, v = kv.partition("=")
+            os.environ[k] = v
         m = UNet(3, 3, compute_dtype=a.dtype)
         m.load_state_dict(sd)
         m = m.to(dev).eval()
