@@ -1,0 +1,74 @@
+"""Multi-GPU through the C-ABI itself: two ranks, each with its own handle on its
+own GPU, run a native forward of their shard into bit-packed masks and exchange them with the
+library's RCCL all-gather (unet_comm_get_unique_id / unet_comm_init / unet_allgather) -- the path a
+C host without torch.distributed takes.  Each rank's gathered batch must equal a single-process
+forward of the whole batch on GPU 0, bit for bit.  Needs two GPUs (skipped on the one-GPU box;
+the gloo tests in test_dist_cpu.py cover the sharding logic there)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _rank(rank, world, uid, x, sd, q):
+    sys.path.insert(0, os.path.join(REPO, "tw-invoice-unet-ocr-llm_amd"))
+    from unet_mi355x import native
+    from unet_mi355x.model import UNet
+    try:
+        dev = torch.device("cuda", rank)
+        torch.cuda.set_device(dev)
+        m = UNet(3, 3, compute_dtype="mixed")
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        m = m.to(dev).eval()
+        h = m.native_handle(dev)
+        n = x.shape[0] // world
+        xs = torch.from_numpy(x[rank * n:(rank + 1) * n]).to(dev)
+        h.reserve(n, x.shape[2], x.shape[3])
+        send = torch.empty((n, 3, x.shape[2], x.shape[3] // 8), dtype=torch.uint8, device=dev)
+        recv = torch.empty((world * n,) + tuple(send.shape[1:]), dtype=torch.uint8, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        h.comm_init(rank, world, uid)
+        h.forward(xs, None, send, native.MASK_BITS, stream)
+        h.allgather(send, recv, stream)
+        torch.cuda.synchronize(dev)
+        h.comm_destroy()
+        q.put((rank, recv.cpu().numpy()))
+        m.close()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (the one-GPU box runs the gloo tests)")
+def test_two_rank_native_forward_and_rccl_allgather():
+    sys.path.insert(0, os.path.join(REPO, "tw-invoice-unet-ocr-llm_amd"))
+    from unet_mi355x import native, synthetic as syn
+    from unet_mi355x.model import UNet
+    world = 2
+    x = syn.invoice_pages(11, 4, 128, 128, 3)
+    sd = {k: np.asarray(v) for k, v in syn.make_state_dict(0, 3, 3, "pretrained").items()}
+    uid = native.Handle.comm_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, world, uid, x, sd, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert not isinstance(got[r], str), got[r]
+    m = UNet(3, 3, compute_dtype="mixed")
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.to("cuda:0").eval()
+    with torch.no_grad():
+        ref = m.forward_masks(torch.from_numpy(x).to("cuda:0"), packed=True).cpu().numpy()
+    m.close()
+    for r in range(world):
+        assert np.array_equal(got[r], ref), f"rank {r}'s gathered masks differ from the one-process forward"

@@ -1267,7 +1267,9 @@ __device__ __forceinline__ void wait_vm_barrier_rt(int n) {
 // HS = 1 (down1.3): down1.0 fused in, as in the 4-wave ring (its halo chunks are computed from a
 // 20 x 36 window of the pre-cast input on 16x16x16 MFMAs); needs WST (the loop then has a barrier
 // after every step: the window is re-filled while the halo of the next tile is computed from it).
-template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0>
+// ABL (timing-only ablation builds, `make abl`): 5 = no tile epilogue (the accumulators are kept
+// alive, nothing is stored) -- the per-tile epilogue's share of a layer, wrong outputs by construction.
+template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a) {
   using G = Ring8Geom<T, TCW, NS, TPS, WST, HS>;
   constexpr int NW = G::NW, TW = G::TW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
@@ -1734,9 +1736,17 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       // tile.  The stores are issued after those loads, so the next step's counted wait (for loads
       // issued after them) retires them under that step's MFMAs.
 #pragma unroll
-      for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<TO, TQ, TP, EPI, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
-                                           tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s, headb_s);
+      for (int h = 0; h < TC / 4; ++h) {
+        if constexpr (ABL == 5) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int p = 0; p < TP; ++p) asm volatile("" ::"v"(acc[4 * h + t][p]));
+        } else {
+          conv_epilogue<TO, TQ, TP, EPI, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
+                                             tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s, headb_s);
+        }
+      }
 #pragma unroll
       for (int t = 0; t < TC; ++t)
 #pragma unroll
@@ -1746,7 +1756,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   }
 }
 
-template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0>
+template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0, int ABL = 0>
 static hipError_t launch_ring8(const IgemmArgs& a, hipStream_t s) {
   using G = Ring8Geom<T, TCW, NS, TPS, WST, HS>;
   if constexpr (HS != 0) {
@@ -1759,7 +1769,7 @@ static hipError_t launch_ring8(const IgemmArgs& a, hipStream_t s) {
   int n_slots = kNumCUs / a.n_ct;   // one 512-thread block per CU
   if (n_slots < 1) n_slots = 1;
   if (n_slots > n_mt) n_slots = n_mt;
-  hipLaunchKernelGGL((conv3x3_ring8_kernel<T, TCW, NS, EPI, TPS, WST, TO, TQ, HS>), dim3(a.n_ct * n_slots), dim3(512),
+  hipLaunchKernelGGL((conv3x3_ring8_kernel<T, TCW, NS, EPI, TPS, WST, TO, TQ, HS, ABL>), dim3(a.n_ct * n_slots), dim3(512),
                      0, s, a);
   return hipGetLastError();
 }
@@ -2114,6 +2124,11 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
       case CFG_RING_FUSED_IN:
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ, ABL>(a, s);
         break;
+      case CFG_RING8_R128:
+        if constexpr (ABL == 5 && EPI != EPI_HEAD) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ, 0, 5>(a, s);
+        break;
+      case CFG_RING8_R64_T9: if constexpr (ABL == 5) return launch_ring8<T, 4, 2, EPI, 9, 0, TO, TQ, 0, 5>(a, s); break;
+      case CFG_RING8_R64_WS: if constexpr (ABL == 5) return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ, 0, 5>(a, s); break;
       default: break;
     }
     return hipErrorInvalidValue;
