@@ -246,6 +246,118 @@ __device__ __forceinline__ float xsum_lane32(float x) {   // x[l] + x[l ^ 32]
 // (the two differ where a layer feeds consumers of different storage type, see unet_capi.cpp).
 // up_out (EPI_UPSCATTER only): scatter into up_out (pixel stride up_ldo, channel offset 0, up_cout
 // channels per (a, b) group) instead of a.out / a.ldo / a.out_off / a.Cout (EPI_UPFUSE).
+// EPI_HEAD: conv1.3 + BN + ReLU kept in fp32, the 64 -> ncls 1x1 out_conv as per-lane FMA chains
+// summed over the wave's four row quads with permlane16/32 swaps (VALU, no LDS round trip), then
+// the logits and / or masks (sigmoid > thr as logit > the host-bisected cut).  Round 3 (the
+// per-layer no-epilogue ablation put this epilogue at 29 % of conv1.3, profiles/
+// tune_r3g_epilogue_ablation.txt): the 1x1 weights are read once per tile instead of per pixel
+// group and class (each read was waited for right before its dot), every class is computed
+// without a branch (classes >= ncls have zero weights here), the mask kind is resolved once per
+// tile (one straight-line loop per kind), and bit-packed masks of a full 16 x 32 tile leave as one
+// dword per (class, row): the wave's TP = 4 pixel groups are one row pair x 32 columns, so each
+// class's ballots assemble into two 32-bit row words in scalar registers.  Same arithmetic per
+// logit (fmaf order, swaps, + bias), so bitwise the same logits and masks.
+template <int TP, int TW>
+__device__ __forceinline__ void head_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0, int ox0,
+                                              int g0, const float (&bv)[16], const float* head_w,
+                                              const float* head_b) {
+  const int H = a.H, W = a.W;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4;
+  const int col = lane & 15;
+  const int ncls = a.ncls;
+  float hw[kMaxClasses][16], hb[kMaxClasses], cut[kMaxClasses];
+#pragma unroll
+  for (int c = 0; c < kMaxClasses; ++c) {
+    const bool live = c < ncls;   // wave-uniform
+    hb[c] = live ? head_b[c] : 0.f;
+    cut[c] = a.thr_logit[c];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 w4 = live ? *reinterpret_cast<const f32x4*>(head_w + c * 64 + q * 16 + 4 * i)
+                            : f32x4{0.f, 0.f, 0.f, 0.f};
+      hw[c][4 * i] = w4[0]; hw[c][4 * i + 1] = w4[1]; hw[c][4 * i + 2] = w4[2]; hw[c][4 * i + 3] = w4[3];
+    }
+  }
+  auto logits_of = [&](int p, float (&logit)[kMaxClasses]) {
+    float v[16];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[t * 4 + e] = relu_nan(acc[t][p][e] + bv[t * 4 + e]);
+#pragma unroll
+    for (int c = 0; c < kMaxClasses; ++c) {
+      float sum = 0.f;
+      if (c < ncls) {   // wave-uniform: a dead class costs a scalar branch, not 16 FMAs + 2 swaps
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sum = fmaf(hw[c][e], v[e], sum);
+        sum = xsum_lane16(sum);
+        sum = xsum_lane32(sum);
+      }
+      logit[c] = sum + hb[c];
+    }
+  };
+  auto pixel = [&](int p, int& oy, int& ox) {
+    int py, px;
+    pix_of_w<TW>((g0 + p) * 16 + col, py, px);
+    oy = oy0 + py;
+    ox = ox0 + px;
+  };
+  const long long plane = (long long)H * W;
+  float* const lg = a.logits;
+  if (a.mask_kind == MASK_BITS && TW == 32 && TP == 4 && (W & 31) == 0 && ox0 + 32 <= W && (g0 & 3) == 0) {
+    unsigned w0[kMaxClasses], w1[kMaxClasses];
+#pragma unroll
+    for (int c = 0; c < kMaxClasses; ++c) w0[c] = w1[c] = 0u;
+#pragma unroll
+    for (int p = 0; p < TP; ++p) {
+      float logit[kMaxClasses];
+      logits_of(p, logit);
+      int oy, ox;
+      pixel(p, oy, ox);
+#pragma unroll
+      for (int c = 0; c < kMaxClasses; ++c) {
+        // group p = bits 8p .. 8p+7 of the pair's row words (lanes q = 0: row col >> 3, column col & 7)
+        const unsigned long long bal = __ballot(logit[c] > cut[c]);
+        w0[c] |= ((unsigned)bal & 0xFFu) << (8 * p);
+        w1[c] |= ((unsigned)(bal >> 8) & 0xFFu) << (8 * p);
+        if (lg && c < ncls && q == 0 && oy < H) lg[(long long)(n * ncls + c) * plane + (long long)oy * W + ox] = logit[c];
+      }
+    }
+    const int oy = oy0 + 2 * (g0 / (TW / 8)) + lane;   // lane r < 2 stores row r of the wave's row pair
+    if (lane < 2 && oy < H) {
+#pragma unroll
+      for (int c = 0; c < kMaxClasses; ++c)
+        if (c < ncls)
+          *reinterpret_cast<unsigned*>(a.masks + ((long long)(n * ncls + c) * H + oy) * (W >> 3) + (ox0 >> 3)) =
+              lane ? w1[c] : w0[c];
+    }
+    return;
+  }
+#pragma unroll
+  for (int p = 0; p < TP; ++p) {
+    float logit[kMaxClasses];
+    logits_of(p, logit);
+    int oy, ox;
+    pixel(p, oy, ox);
+    const bool inside = oy < H && ox < W;
+#pragma unroll
+    for (int c = 0; c < kMaxClasses; ++c) {
+      if (c >= ncls) break;
+      const long long pix = (long long)(n * ncls + c) * plane + (long long)oy * W + ox;
+      if (lg && q == 0 && inside) lg[pix] = logit[c];
+      const bool on = logit[c] > cut[c];
+      if (a.mask_kind == MASK_U8) {
+        if (q == 0 && inside) a.masks[pix] = on ? 1 : 0;
+      } else if (a.mask_kind == MASK_BITS) {
+        const unsigned long long bal = __ballot(on);
+        if (q == 0 && (col & 7) == 0 && inside)
+          a.masks[((long long)(n * ncls + c) * H + oy) * (W >> 3) + (ox >> 3)] = (uint8_t)((bal >> (col & 8)) & 0xFFu);
+      }
+    }
+  }
+}
+
 template <typename TO, typename TQ, int TP, int EPI, int TW = 16, int NOSTORE = 0>
 __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0,
                                               int ox0, int g0, int row0, const float* bias_w,
@@ -263,6 +375,10 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
   for (int i = 0; i < 4; ++i) {
     const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias_w + q * 16 + 4 * i);
     bv[4 * i] = b4[0]; bv[4 * i + 1] = b4[1]; bv[4 * i + 2] = b4[2]; bv[4 * i + 3] = b4[3];
+  }
+  if constexpr (EPI == EPI_HEAD && !NOSTORE) {
+    head_epilogue<TP, TW>(a, acc, n, oy0, ox0, g0, bv, head_w, head_b);
+    return;
   }
 
 #pragma unroll
@@ -320,44 +436,7 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
                          : reinterpret_cast<TO*>(a.out) + ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0;
         store64_grouped<TO>(grp, v);
       }
-    } else {  // EPI_HEAD: 1x1 conv 64 -> ncls on the fp32 activations, then masks
-      // All class dots first (independent FMA chains), then the 4 row-quads of the
-      // wave are summed with permlane16/32 swaps (VALU, no LDS round trip).
-      float logit[kMaxClasses];
-#pragma unroll
-      for (int c = 0; c < kMaxClasses; ++c) {
-        float sum = 0.f;
-        if (c < a.ncls) {
-          const float* hw = head_w + c * 64 + q * 16;
-#pragma unroll
-          for (int e = 0; e < 16; ++e) sum = fmaf(hw[e], v[e], sum);
-          sum = xsum_lane16(sum);
-          sum = xsum_lane32(sum);
-          sum += head_b[c];
-        }
-        logit[c] = sum;
-      }
-#pragma unroll
-      for (int c = 0; c < kMaxClasses; ++c) {
-        if (c >= a.ncls) break;
-        const long long pix = ((long long)(n * a.ncls + c) * H + oy) * W + ox;
-        if (a.logits && q == 0 && inside) a.logits[pix] = logit[c];
-        if (a.mask_kind != MASK_NONE) {
-          // sigmoid(logit) > thr (inference.py:72-78, strict '>') == logit > thr_logit[c]:
-          // the host bisects the fp32 sigmoid for the exact logit cut (unet_capi.cpp).
-          const bool on = logit[c] > a.thr_logit[c];
-          if (a.mask_kind == MASK_U8) {
-            if (q == 0 && inside) a.masks[pix] = on ? 1 : 0;
-          } else {
-            const unsigned long long bal = __ballot(on);
-            if (q == 0 && (col & 7) == 0 && inside) {
-              const unsigned byte = (unsigned)(bal >> (col & 8)) & 0xFFu;
-              a.masks[((long long)(n * a.ncls + c) * H + oy) * (W >> 3) + (ox >> 3)] = (uint8_t)byte;
-            }
-          }
-        }
-      }
-    }
+    }   // EPI_HEAD: head_epilogue above
   }
 }
 
