@@ -415,10 +415,13 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
         float m[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          // 2x2 window partners are lanes ^1 (quad_perm [1,0,3,2]) and ^8 (row_ror:8):
-          // DPP moves instead of ds_bpermute round trips through LDS.
-          const float o = max_nan(v[e], dpp_f32<0xB1>(v[e]));
-          m[e] = max_nan(o, dpp_f32<0x128>(o));
+          // 2x2 window partners are lanes ^1 (quad_perm [1,0,3,2]) and ^8 (row_ror:8).  The values
+          // are ReLU outputs (+0 .. +inf or NaN), whose fp32 order is their unsigned bit-pattern
+          // order, NaN (either sign) above all: an unsigned max with the DPP move folded into it
+          // (one v_max_u32_dpp per partner) is MaxPool2d's max with its NaN propagation.
+          const unsigned u = __float_as_uint(v[e]);
+          const unsigned o = max(u, (unsigned)__builtin_amdgcn_update_dpp(0, (int)u, 0x128, 0xF, 0xF, true));
+          m[e] = __uint_as_float(max(o, (unsigned)__builtin_amdgcn_update_dpp(0, (int)o, 0xB1, 0xF, 0xF, true)));
         }
         if ((col & 9) == 0 && oy + 1 < H && ox + 1 < W) {
           const int Ho = H >> 1, Wo = W >> 1;
