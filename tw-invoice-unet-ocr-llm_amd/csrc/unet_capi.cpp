@@ -674,7 +674,9 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     // keep every layer on a configuration it supports, within the same kernel family (the
     // configurations of a family accumulate in the same K order, so they agree bitwise)
     const bool ring = cfg_is_ring(c);
-    if (cfg_fused_in(c) && (i != D1B || f32)) c = L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128;
+    if (cfg_fused_in(c) && (i != D1B || f32))   // the same ring family on the other layers
+      c = cfg_is_ring8(c) ? (L.cout == 64 ? CFG_RING8_R64_T9 : CFG_RING8_R128)
+                          : (L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128);
     if (c == CFG_RING8_R64_WS && (L.cin != 64 || f32)) c = L.cout == 64 ? CFG_RING8_R64_T9 : CFG_RING8_R128;   // 72 KB of weights max
     if (c == CFG_RING8_R128 && L.cout == 64) c = CFG_RING8_R64_T9;
     if (c == CFG_RING_R64_W12 && f32) c = CFG_RING_R64_T3;   // 16-bit only

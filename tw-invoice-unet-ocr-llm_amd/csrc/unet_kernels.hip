@@ -257,7 +257,7 @@ __device__ __forceinline__ float xsum_lane32(float x) {   // x[l] + x[l ^ 32]
 // dword per (class, row): the wave's TP = 4 pixel groups are one row pair x 32 columns, so each
 // class's ballots assemble into two 32-bit row words in scalar registers.  Same arithmetic per
 // logit (fmaf order, swaps, + bias), so bitwise the same logits and masks.
-template <int TP, int TW>
+template <int TP, int TW, int BACC>
 __device__ __forceinline__ void head_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0, int ox0,
                                               int g0, const float (&bv)[16], const float* head_w,
                                               const float* head_b) {
@@ -284,7 +284,7 @@ __device__ __forceinline__ void head_epilogue(const IgemmArgs& a, const f32x4 (&
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[t * 4 + e] = relu_nan(acc[t][p][e] + bv[t * 4 + e]);
+      for (int e = 0; e < 4; ++e) v[t * 4 + e] = relu_nan(BACC ? acc[t][p][e] : acc[t][p][e] + bv[t * 4 + e]);
 #pragma unroll
     for (int c = 0; c < kMaxClasses; ++c) {
       float sum = 0.f;
@@ -358,7 +358,9 @@ __device__ __forceinline__ void head_epilogue(const IgemmArgs& a, const f32x4 (&
   }
 }
 
-template <typename TO, typename TQ, int TP, int EPI, int TW = 16, int NOSTORE = 0>
+// BACC = 1: the accumulators already hold the bias (the 8-wave ring starts every tile's
+// accumulators at the bias instead of zero, init_acc_bias), so no bias add here.
+template <typename TO, typename TQ, int TP, int EPI, int TW = 16, int NOSTORE = 0, int BACC = 0>
 __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0,
                                               int ox0, int g0, int row0, const float* bias_w,
                                               const float* head_w, const float* head_b,
@@ -373,11 +375,12 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
   float bv[16];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias_w + q * 16 + 4 * i);
+    f32x4 b4 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (!BACC) b4 = *reinterpret_cast<const f32x4*>(bias_w + q * 16 + 4 * i);
     bv[4 * i] = b4[0]; bv[4 * i + 1] = b4[1]; bv[4 * i + 2] = b4[2]; bv[4 * i + 3] = b4[3];
   }
   if constexpr (EPI == EPI_HEAD && !NOSTORE) {
-    head_epilogue<TP, TW>(a, acc, n, oy0, ox0, g0, bv, head_w, head_b);
+    head_epilogue<TP, TW, BACC>(a, acc, n, oy0, ox0, g0, bv, head_w, head_b);
     return;
   }
 
@@ -392,7 +395,7 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
     for (int t = 0; t < TC; ++t)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float x = acc[t][p][e] + bv[t * 4 + e];
+        float x = BACC ? acc[t][p][e] : acc[t][p][e] + bv[t * 4 + e];
         if (EPI != EPI_UPSCATTER) x = relu_nan(x);
         v[t * 4 + e] = x;
       }
@@ -1459,12 +1462,20 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   };
 
   f32x4 acc[TC][TP];
-#pragma unroll
-  for (int t = 0; t < TC; ++t)
-#pragma unroll
-    for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   const int col = lane & 15, q = lane >> 4;
+  // Every tile's accumulators start at the layer bias (rows 64h + 16q + 4t + e of the lane, the packed
+  // row permutation) instead of zero: the same number of register moves as the zeroing, and the
+  // epilogue loses its bias add (one VALU op per output value).  bias_s must be visible (written in
+  // the prologue, before its barrier).
+  auto init_acc_bias = [&](int t0, int t1) {
+#pragma unroll
+    for (int t = 0; t < TC; ++t) {
+      if (t < t0 || t >= t1) continue;
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias_s + 64 * (t / 4) + 16 * q + 4 * (t % 4));
+#pragma unroll
+      for (int p = 0; p < TP; ++p) acc[t][p] = b4;
+    }
+  };
   int prow[TP];
 #pragma unroll
   for (int p = 0; p < TP; ++p) {
@@ -1586,6 +1597,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     const int young = total - 1 < NS - 2 ? total - 1 : NS - 2;   // W(1..NS-2) may stay in flight
     wait_vm_barrier_rt(young * wcnt);
   }
+  init_acc_bias(0, TC);
 
   auto step = [&](int g, int hs, int tp, int tsub) {
     const int dy = tp / 3, dx = tp - (tp / 3) * 3;
@@ -1652,12 +1664,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       tile_of(item, n, ty, tx);
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<TO, TQ, TP, EPI, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
-                                           tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s, headb_s);
-#pragma unroll
-      for (int t = 0; t < TC; ++t)
-#pragma unroll
-        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+        conv_epilogue<TO, TQ, TP, EPI, TW, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
+                                                 tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s, headb_s);
+      init_acc_bias(0, TC);
     }
     return;
   }
@@ -1669,14 +1678,11 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          float bv[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) bv[j] = bias_s[64 * h + 16 * q + 8 * half + j];
-#pragma unroll
-          for (int p = 0; p < TP; ++p) {
+          for (int p = 0; p < TP; ++p) {   // the accumulators hold the bias (init_acc_bias)
             t8 v;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = (T)relu_nan(acc[4 * h + 2 * half + (j >> 2)][p][j & 3] + bv[j]);
+            for (int j = 0; j < 8; ++j) v[j] = (T)relu_nan(acc[4 * h + 2 * half + (j >> 2)][p][j & 3]);
             xb[p][2 * h + half] = __builtin_bit_cast(frag_t, v);
           }
         }
@@ -1803,10 +1809,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 #pragma unroll
           for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-#pragma unroll
-      for (int t = 4; t < TC; ++t)
-#pragma unroll
-        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      init_acc_bias(0, TC);   // the next tile's conv accumulators (acc[0..3] held the ConvTranspose quadrants)
       ++item;
       continue;
     }
@@ -1825,14 +1828,12 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 #pragma unroll
             for (int p = 0; p < TP; ++p) asm volatile("" ::"v"(acc[4 * h + t][p]));
         } else {
-          conv_epilogue<TO, TQ, TP, EPI, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
-                                             tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s, headb_s);
+          conv_epilogue<TO, TQ, TP, EPI, TW, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
+                                                   tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s,
+                                                   headb_s);
         }
       }
-#pragma unroll
-      for (int t = 0; t < TC; ++t)
-#pragma unroll
-        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      init_acc_bias(0, TC);
       ++item;
     }
   }
