@@ -396,8 +396,8 @@ def kernel_table(runner, model, x, masks, B, S, C, dtype, traffic_json):
     peak = PEAK_TFLOPS[dtype]
     traffic, source = None, None
     if traffic_json == "auto":
-        traffic_json = os.path.join(REPO, "profiles", f"pmc_{dtype}_bs{B}.json")
-    if traffic_json and os.path.exists(traffic_json) and S == 512:
+        traffic_json = os.path.join(REPO, "profiles", f"pmc_{dtype}_bs{B}" + ("" if S == 512 else f"_{S}") + ".json")
+    if traffic_json and os.path.exists(traffic_json):
         tj = json.load(open(traffic_json))
         traffic = tj.get(dom_name, {}).get("hbm_bytes_per_launch")
         meta = tj.get("_meta", {})

@@ -39,3 +39,19 @@ python tools/pmc_summary.py gpurun_out/pmc_$TAG --bench-json gpurun_out/prof_ben
     --out gpurun_out/pmc_$TAG/summary.json > gpurun_out/pmc_$TAG/summary.txt
 python tools/prof_summary.py gpurun_out/prof_$TAG/run_kernel_trace.csv --min-grid 10000 > gpurun_out/prof_$TAG/summary.txt
 echo summaries ok
+# BASELINE config 5 (1024^2, fp16, bs64): kernel stats + the same PMC passes
+C5="--size 1024 --batch 64 --dtype fp16 $P"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_cfg5 -o run -- \
+    python3 bench.py --steps 3 --warmup 1 $C5 > gpurun_out/prof_bench_${TAG}_cfg5.json 2> gpurun_out/prof_${TAG}_cfg5.err
+mkdir -p gpurun_out/pmc_${TAG}_cfg5
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/pmc_${TAG}_cfg5/pass$i -o run -- \
+      python3 bench.py --steps 1 --warmup 0 --no-layer-profile $C5 > gpurun_out/pmc_${TAG}_cfg5/pass$i.log 2>&1
+done
+python tools/pmc_summary.py gpurun_out/pmc_${TAG}_cfg5 --batch 64 --size 1024 --bench-json gpurun_out/prof_bench_${TAG}_cfg5.json \
+    --commit $COMMIT --out gpurun_out/pmc_${TAG}_cfg5/summary.json > gpurun_out/pmc_${TAG}_cfg5/summary.txt
+python tools/prof_summary.py gpurun_out/prof_${TAG}_cfg5/run_kernel_trace.csv --min-grid 10000 > gpurun_out/prof_${TAG}_cfg5/summary.txt
+echo cfg5 profiles ok
