@@ -340,11 +340,15 @@ def make_leg(runner, rank, world, n_total, per_rank, seed, S, C, dev, chunk):
 def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
     """The bench contract's timing loop (udist.timed_steps): barrier + sync on both sides, the MAX
     over ranks; optional per-step GPU times (HIP events on this stream) as a diagnostic."""
-    for _ in range(warmup):
-        leg["step"]()
     ev = None
     if per_step_events:
+        # created and recorded once before the warmup: torch creates the HIP events lazily at their first
+        # record, which would otherwise happen inside the timed steps
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        for e in ev:
+            e.record()
+    for _ in range(warmup):
+        leg["step"]()
     marks = iter(ev[1:]) if ev else iter(())
 
     def timed_step():

@@ -503,7 +503,7 @@ std::string layer_label(const Layer& L, int epi) {
                   cfg == CFG_TRING_R256 ? 2 : 1, tname(L.dto));
   } else if (cfg_is_ring8(cfg)) {
     const int wst = cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;   // weight-stationary
-    std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, %d, %d, %d, %d, %d, %s, %s, %d>", tname(L.dt),
+    std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, %d, %d, %d, %d, %d, %s, %s, %d, 0>", tname(L.dt),
                   cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), wst, tname(L.dto),
                   tname(epi == EPI_POOL ? L.dtq : L.dto), cfg == CFG_RING8_FUSED_IN ? 1 : 0);
   } else if (cfg_is_ring(cfg)) {
