@@ -8,12 +8,15 @@ The fused first conv writes each 32-channel halo chunk with ds_write_b128 (lane 
 (a/4) mod 64.  Cost = LDS cycles relative to a conflict-free access (1.0 = none).
 
 Findings (printed):
-  1. today's layout (quarter q of halo pixel (hy, hx) at q ^ (hx & 3)): reads 1.0, writes 2.08;
+  1. the round-2 layout (quarter q of halo pixel (hy, hx) at q ^ (hx & 3), 16 row-consecutive
+     pixels per group): reads 1.0, writes 2.08;
   2. no XOR table sw(hy mod 2, hx mod 8) keeps the reads conflict-free while 8 consecutive
      pixels of one halo row write conflict-free (exhaustive over the write-admissible tables);
-  3. sw = (hx & 3) ^ (hy & 1) with write groups of 2 rows x 4 pixels: reads 1.0, writes 1.04 --
-     but the first conv's window reads (ds_read_b64, 2 rows per 16 lanes, 288-B row stride)
-     then conflict instead, and the window stride cannot grow (down1.3 uses all 160 KiB of LDS).
+  3. sw = (hx & 3) ^ (hy & 1) with write groups of 2 adjacent rows x 4 pixels: reads 1.0, writes
+     1.04 -- but the first conv's window reads (ds_read_b64, 2 rows per 16 lanes, 288-B row stride)
+     then conflict instead (1.92), and the window stride cannot grow (down1.3 uses all 160 KiB);
+  4. the kernel's layout: the same swizzle with the two rows of a write group 3 apart (3 x 288 B
+     = 96 mod 256): tap reads 1.0, halo writes 1.04 (the last two columns), window reads 1.0.
 
     python tools/halo_swizzle_search.py
 """
@@ -70,14 +73,20 @@ def rowwise(grp, c):
     return None if p >= HP else divmod(p, HWD)
 
 
-def two_row(grp, c):
-    """16 pixels = 2 rows x 8 (lanes 0-3 / 4-7: rows hy / hy+1 at hx 0-3; lanes 8-15 at hx 4-7);
-    the last two halo columns in 3 groups of 2-column runs."""
+def two_row(grp, c, gap=1):
+    """16 pixels = 2 rows x 8 (lanes 0-3 / 4-7: rows hy / hy+gap at hx 0-3; lanes 8-15 at hx 4-7);
+    the last two halo columns in 3 groups of 2-column runs.  gap = 3 is the kernel's mapping
+    (compute_halo in conv3x3_ring8_kernel, HS = 1): row pairs (0,3) (1,4) (2,5) (6,9) ... (14,17)."""
     if grp < 36:
         rp, cg = grp // 4, grp % 4
-        return 2 * rp + ((c >> 2) & 1), 8 * cg + (c & 3) + 4 * (c >> 3)
+        base = 2 * rp if gap == 1 else 6 * (rp // 3) + rp % 3
+        return base + gap * ((c >> 2) & 1), 8 * cg + (c & 3) + 4 * (c >> 3)
     k = (grp - 36) * 16 + c
     return None if k >= 36 else (k // 2, 32 + (k & 1))
+
+
+def kernel_map(grp, c):
+    return two_row(grp, c, gap=3)
 
 
 def halo_writes(sw, pix):
@@ -145,14 +154,16 @@ def reads_ok(ra, rb, apar):
 
 def main():
     cur = lambda hy, hx: hx & 3  # noqa: E731
-    print(f"1. current: tap reads {tap_reads(cur):.3f}, halo writes {halo_writes(cur, rowwise):.3f}, "
+    print(f"1. round 2: tap reads {tap_reads(cur):.3f}, halo writes {halo_writes(cur, rowwise):.3f}, "
           f"window reads {window_reads(rowwise):.3f}")
     rows = list(write_admissible_rows())
     n = sum(reads_ok(ra, rb, par) for ra in rows for rb in rows for par in (0, 1))
     print(f"2. write-admissible row tables: {len(rows)}; (row a, row a+1) pairs with conflict-free reads: {n}")
     alt = lambda hy, hx: (hx & 3) ^ (hy & 1)  # noqa: E731
-    print(f"3. sw = (hx&3)^(hy&1), 2-row write groups: tap reads {tap_reads(alt):.3f}, "
+    print(f"3. sw = (hx&3)^(hy&1), write groups of rows (hy, hy+1): tap reads {tap_reads(alt):.3f}, "
           f"halo writes {halo_writes(alt, two_row):.3f}, window reads {window_reads(two_row):.3f}")
+    print(f"4. the kernel's: sw = (hx&3)^(hy&1), rows (hy, hy+3): tap reads {tap_reads(alt):.3f}, "
+          f"halo writes {halo_writes(alt, kernel_map):.3f}, window reads {window_reads(kernel_map):.3f}")
 
 
 if __name__ == "__main__":
