@@ -28,6 +28,7 @@ and at the bench plan), kernels (per-instantiation time breakdown).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import re
@@ -340,6 +341,11 @@ def make_leg(runner, rank, world, n_total, per_rank, seed, S, C, dev, chunk):
 def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
     """The bench contract's timing loop (udist.timed_steps): barrier + sync on both sides, the MAX
     over ranks; optional per-step GPU times (HIP events on this stream) as a diagnostic."""
+    # no Python garbage collection inside the timed steps (timeit's practice): a collection pass over
+    # torch's and numpy's objects pauses the launching thread for milliseconds, and the GPU idles
+    gc.collect()
+    gc_was_enabled = gc.isenabled()
+    gc.disable()
     ev = None
     if per_step_events:
         # created and recorded once before the warmup: torch creates the HIP events lazily at their first
@@ -359,7 +365,11 @@ def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
     if ev:
         sync()
         ev[0].record()
-    elapsed, host = udist.timed_steps(timed_step, steps, 0, sync=sync, device=dev)
+    try:
+        elapsed, host = udist.timed_steps(timed_step, steps, 0, sync=sync, device=dev)
+    finally:
+        if gc_was_enabled:
+            gc.enable()
     out = {"elapsed": elapsed, "ms_per_step": 1e3 * elapsed / steps,
            "value": leg["n_total"] * steps / elapsed, "host_step_ms": [round(1e3 * t, 3) for t in host]}
     if ev:
