@@ -1333,8 +1333,6 @@ struct Ring8Geom {
   static constexpr int LDS_BYTES = XS_OFF + XS_BYTES;          // HS: exactly 160 KiB
 };
 
-template <int N>
-__device__ __forceinline__ void wait_vm_barrier_rt_case() { wait_vm_barrier<N>(); }
 // vmcnt(n) + barrier for a runtime (wave-uniform) n in [0, 15]
 __device__ __forceinline__ void wait_vm_barrier_rt(int n) {
   switch (n) {
@@ -1526,22 +1524,44 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       toff[m] = ((ta / 3) * G::XW + ta % 3) * 4 * (int)sizeof(T) + (first_tap(4 * m + (lane >> 4)) > 8 ? 1 : 0);
     }
   }
+  // The computed halo's LDS image: quarter q of halo pixel (hy, hx) at q ^ (hx & 3) ^ (hy & 1) (the
+  // DMA'd halo of the other layers has no hy term).  A 16-pixel group of the halo computation is
+  // 2 rows x 8 pixels, rows (hy, hy + 3) -- lanes 0-3 / 4-7 at hx 0-3, 8-11 / 12-15 at hx 4-7 --
+  // so that every 8-lane group of its ds_write_b128 covers 8 distinct 16-byte slots of a 128-byte
+  // bank row (consecutive pixels of one row cover 4: 2-way conflicted, 10.5 % of the layer's LDS
+  // cycles in r2p), while the taps' ds_read_b128 and the window's ds_read_b64 (the two rows
+  // 3 x 288 B apart) stay conflict-free; the last two halo columns (36 pixels) follow in 3 groups
+  // of row-consecutive pairs.  Rows paired: (0,3) (1,4) (2,5) (6,9) ... (14,17).
+  // tools/halo_swizzle_search.py: no XOR table makes row-consecutive writes conflict-free as well.
   constexpr int HGR = (HP + 15) / 16;                     // 16-pixel groups of the halo
   constexpr int HIT = (HGR + 2 * NW - 1) / (2 * NW);      // groups per wave and part
-  auto compute_halo = [&](int i, int cb, int hb, int part) {
+  static_assert(HS == 0 || (HWD == 34 && HGR == 39), "computed halo groups: 9 row pairs x 4 + 3");
+  // cb (the 32-channel chunk: selects w0f / b0v) and part are compile-time (std::integral_constant):
+  // with runtime values the two register arrays are indexed dynamically and go to scratch.
+  auto compute_halo = [&](int i, auto cbc, int hb, auto partc) {
+    constexpr int cb = decltype(cbc)::value, part = decltype(partc)::value;
     if constexpr (HS != 0) {
       int n, ty, tx;
       tile_of(i, n, ty, tx);
       const char* xs = lds + G::XS_OFF + (i & 1) * G::XS1;
       char* dst = lds + hb * HALO_BYTES;
-      const int qq = lane >> 4;
+      const int qq = lane >> 4, c = lane & 15;
 #pragma unroll
       for (int it = 0; it < HIT; ++it) {
         const int grp = wave + part * NW + it * 2 * NW;
         if (grp >= HGR) break;   // wave-uniform
-        const int p = grp * 16 + (lane & 15);
-        const bool real = p < HP;
-        const int hy = real ? p / HWD : 0, hx = real ? p - (p / HWD) * HWD : 0;
+        bool real = true;
+        int hy, hx;
+        if (grp < 36) {          // wave-uniform
+          const int rp = grp >> 2;
+          hy = 6 * (rp / 3) + rp % 3 + 3 * ((c >> 2) & 1);
+          hx = 8 * (grp & 3) + (c & 3) + 4 * (c >> 3);
+        } else {
+          const int k = (grp - 36) * 16 + c;
+          real = k < 36;
+          hy = real ? k >> 1 : 0;
+          hx = 32 + (k & 1);
+        }
         const char* px = xs + (hy * G::XW + hx) * 4 * (int)sizeof(T);
         f32x4 acc0[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -1559,17 +1579,21 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[4 * t + e] = (T)(inimg ? relu_nan(acc0[t][e] + b0v[cb][4 * t + e]) : 0.f);
-        if (real) *reinterpret_cast<uint4*>(dst + p * 64 + ((qq ^ (hx & 3)) << 4)) = __builtin_bit_cast(uint4, o);
+        if (real)
+          *reinterpret_cast<uint4*>(dst + (hy * HWD + hx) * 64 + ((qq ^ (hx & 3) ^ (hy & 1)) << 4)) =
+              __builtin_bit_cast(uint4, o);
       }
     }
   };
 
   // prologue: halo of chunk 0; weights (all steps, or steps 0 .. NS-2); epilogue parameters
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
   if constexpr (HS != 0) {
     issue_xs(0);
     wait_vm_barrier<0>();
-    compute_halo(0, 0, 0, 0);
-    compute_halo(0, 0, 0, 1);
+    compute_halo(0, C0{}, 0, C0{});
+    compute_halo(0, C0{}, 0, C1{});
   } else {
     issue_halo();
   }
@@ -1640,25 +1664,26 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       const char* hs9[9];
       const char* ws9[9];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) {
+      for (int k = 0; k < 9; ++k) {   // halo row of the lane's pixel: (col >> 3) + row (mod 2)
         const int row = k / 3, dx = k % 3;
-        hs9[k] = lds + ch * HALO_BYTES + (row * HWD + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
+        hs9[k] = lds + ch * HALO_BYTES + (row * HWD + dx) * 64 +
+                 ((q ^ ((px_lane + dx) & 3) ^ (((col >> 3) + row) & 1)) << 4);
         ws9[k] = wrow + (ch * 3 + row) * SLOT + dx * WSLOT;
       }
       mfma_taps<T, TC, TP, 9>(acc, hs9, ws9, prow);
     };
-    auto halo_all = [&](int i, int cb) {   // both halves of chunk cb of tile i -> buffer cb
-      compute_halo(i, cb, cb, 0);
-      compute_halo(i, cb, cb, 1);
+    auto halo_all = [&](int i, auto cbc) {   // both halves of chunk cb of tile i -> buffer cb
+      compute_halo(i, cbc, decltype(cbc)::value, C0{});
+      compute_halo(i, cbc, decltype(cbc)::value, C1{});
     };
     for (int item = 0; item < items; ++item) {
       const bool more = item + 1 < items;
       if (more) issue_xs(item + 1);
       taps9(0);
-      halo_all(item, 1);
+      halo_all(item, C1{});
       wait_vm_barrier<0>();
       taps9(1);
-      if (more) halo_all(item + 1, 0);
+      if (more) halo_all(item + 1, C0{});
       wait_vm_barrier<63>();   // barrier only: no load is waited for here
       int n, ty, tx;
       tile_of(item, n, ty, tx);
@@ -1671,6 +1696,16 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     return;
   }
   frag_t xb[UPF ? TP : 1][UPF ? 4 : 1];   // EPI_UPFUSE: see ring_body
+  // EPI_UPFUSE: quadrant quad's accumulators (acc[0..3]) start at the ConvTranspose bias of its 64
+  // rows (headw_s + 64 quad, rows 16q + 4t + e of the lane), so its scatter epilogue adds none
+  auto init_up_bias = [&](int quad) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(headw_s + 64 * quad + 16 * q + 4 * t);
+#pragma unroll
+      for (int p = 0; p < TP; ++p) acc[t][p] = b4;
+    }
+  };
   auto conv_to_xb = [&]() {
     if constexpr (UPF) {
       typedef T t8 __attribute__((ext_vector_type(8)));
@@ -1686,10 +1721,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
             xb[p][2 * h + half] = __builtin_bit_cast(frag_t, v);
           }
         }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      init_up_bias(0);
     }
   };
   auto stepT = [&](int g) {   // one quadrant: acc[t] += A(kb, t) x xb[kb], kb = 0..3 (the ring's K order)
@@ -1801,13 +1833,10 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }
         else wait_vm_barrier_rt(young * wcnt);   // the last halo issue is older than W(g+1)
         // no vmcnt(0) drain: the stores retire under the next step's wait (see ring_body)
-        conv_epilogue<TO, TO, TP, EPI_UPSCATTER, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[0]), n, ty * 16,
-                                                     tx * TW, wp * TP, 64 * quad, headw_s + 64 * quad, nullptr,
-                                                     nullptr, a.out2, a.ldo2, a.Cout / 2);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+        conv_epilogue<TO, TO, TP, EPI_UPSCATTER, TW, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[0]), n,
+                                                           ty * 16, tx * TW, wp * TP, 64 * quad, nullptr, nullptr,
+                                                           nullptr, a.out2, a.ldo2, a.Cout / 2);
+        init_up_bias((quad + 1) & 3);   // (after the last quadrant: overwritten by init_acc_bias below)
       }
       init_acc_bias(0, TC);   // the next tile's conv accumulators (acc[0..3] held the ConvTranspose quadrants)
       ++item;
@@ -1934,12 +1963,19 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
     }
   };
 
+  // Every tile's accumulators start at the ConvTranspose bias (rows wr*16*TC + 64h + 16q + 4t + e of
+  // the lane, the packed row permutation) instead of zero, as in the 8-wave ring: the epilogue
+  // loses its bias add.  bias_s is visible after the prologue's barrier.
   f32x4 acc[TC][TP];
-#pragma unroll
-  for (int t = 0; t < TC; ++t)
-#pragma unroll
-    for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int col = lane & 15, q = lane >> 4;
+  auto init_acc_bias = [&]() {
+#pragma unroll
+    for (int t = 0; t < TC; ++t) {
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias_s + wr * 16 * TC + 64 * (t / 4) + 16 * q + 4 * (t % 4));
+#pragma unroll
+      for (int p = 0; p < TP; ++p) acc[t][p] = b4;
+    }
+  };
   int prow[TP];
 #pragma unroll
   for (int p = 0; p < TP; ++p) {
@@ -1957,6 +1993,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
     const int young = total - 1 < NS - 2 ? total - 1 : NS - 2;
     if (young == 2) wait_vm_barrier<2 * (WI + BI)>(); else if (young == 1) wait_vm_barrier<WI + BI>(); else wait_vm_barrier<0>();
   }
+  init_acc_bias();
 
   int c = 0, item = 0, wskip = 0;
   for (int g = 0; g < total; ++g) {
@@ -1998,14 +2035,10 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
       }
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<TO, TO, TP, EPI_UPSCATTER>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
-                                            tx * 16, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
-                                            bias_s + wr * 16 * TC + 64 * h, nullptr,
-                                            nullptr);
-#pragma unroll
-      for (int t = 0; t < TC; ++t)
-#pragma unroll
-        for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+        conv_epilogue<TO, TO, TP, EPI_UPSCATTER, 16, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n,
+                                                         ty * 16, tx * 16, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
+                                                         nullptr, nullptr, nullptr);
+      init_acc_bias();
       ++item;
     }
   }
@@ -2457,9 +2490,35 @@ template <typename T>
 __global__ __launch_bounds__(256) void x_to_px4_kernel(const void* __restrict__ x, int layout, int xdt, int N, int C,
                                                       int H, int W, T* __restrict__ out) {
   const long long HW = (long long)H * W, P = (long long)N * HW;
+  typedef T t4 __attribute__((ext_vector_type(4)));
+  typedef T t8 __attribute__((ext_vector_type(8)));
+  if (layout == 0 && xdt == 0 && C <= 3 && HW % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) {
+    // the common case (fp32 NCHW: bench.py, run_unet's preprocess output): four pixels per thread,
+    // one 16-byte load per channel plane and two 16-byte stores (4-byte loads and 8-byte stores ran
+    // at 3.9 TB/s); the same casts, so bitwise equal to the generic loop below
+    const float* xf = static_cast<const float*>(x);
+    const long long quads = P / 4;
+    for (long long qd = (long long)blockIdx.x * 256 + threadIdx.x; qd < quads; qd += (long long)gridDim.x * 256) {
+      const long long i = 4 * qd, n = i / HW, hw = i - n * HW;   // HW % 4 == 0: one image per quad
+      float4 v[3] = {};
+      for (int c = 0; c < C; ++c) v[c] = *reinterpret_cast<const float4*>(xf + (n * C + c) * HW + hw);
+      t8 o0, o1;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 vc = v[c < 3 ? c : 0];
+        const bool live = c < C;
+        o0[c] = (T)(live ? vc.x : 0.f);
+        o0[4 + c] = (T)(live ? vc.y : 0.f);
+        o1[c] = (T)(live ? vc.z : 0.f);
+        o1[4 + c] = (T)(live ? vc.w : 0.f);
+      }
+      reinterpret_cast<t8*>(out)[2 * qd] = o0;
+      reinterpret_cast<t8*>(out)[2 * qd + 1] = o1;
+    }
+    return;
+  }
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < P; i += (long long)gridDim.x * 256) {
     const long long n = i / HW, hw = i - n * HW;
-    typedef T t4 __attribute__((ext_vector_type(4)));
     t4 v;
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] = (T)(c < C ? input_at(x, layout, xdt, n, c, hw, C, HW) : 0.f);
