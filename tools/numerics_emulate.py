@@ -84,8 +84,10 @@ def fold(sd, blk, ci):
     return (w * s[:, None, None, None]).float(), ((b - mu) * s + be).float()
 
 
-def emulate(sd, x, plan):
-    """Logits of the emulated native forward (fp32 NCHW)."""
+def emulate(sd, x, plan, head=None):
+    """Logits of the emulated native forward (fp32 NCHW).  head = "fp16" / "bf16": the 1x1 head's
+    operands (conv1.3's ReLU outputs and the out_conv weights) rounded to that type, fp32
+    accumulation and bias (a head on 16-bit MFMAs); None: the fp32 head."""
     def conv(name, h, out_dt):
         blk, ci = name.split(".")
         w, b = fold(sd, blk, ci)
@@ -130,6 +132,8 @@ def emulate(sd, x, plan):
         c8 = conv("conv1.3", a, None)              # fp32 accumulators -> fused head
         hw = torch.from_numpy(np.asarray(sd["out_conv.weight"]))
         hb = torch.from_numpy(np.asarray(sd["out_conv.bias"]))
+        if head is not None:
+            c8, hw = rnd(c8, head), rnd(hw, head)
         return F.conv2d(c8, hw, hb)
 
 
@@ -139,6 +143,7 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--plans", nargs="+", default=["bf16", "fp16", "bf16_l0dec16"])
     ap.add_argument("--weights", default="pretrained")
+    ap.add_argument("--head", nargs="+", default=["fp32"], help="head operand types to emulate (fp32 fp16 bf16)")
     a = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 1)
     sys.path.insert(0, REPO)
@@ -151,11 +156,11 @@ def main():
         lg = orc.unet_forward(sd, x[i:i + 1]).numpy()[0]
         refs.append((lg, orc.masks_from_logits(lg)))
     print(f"oracle: {time.time() - t0:.1f}s", flush=True)
-    for pn in a.plans:
+    for pn, hd in [(p, h) for p in a.plans for h in a.head]:
         plan = plan_of(pn)
         ious, errs, worst = [], [], None
         for i in range(a.images):
-            lg = emulate(sd, x[i:i + 1], plan).numpy()[0]
+            lg = emulate(sd, x[i:i + 1], plan, None if hd == "fp32" else hd).numpy()[0]
             m = orc.masks_from_logits(lg)
             errs.append(float(np.abs(lg - refs[i][0]).max()))
             for f in orc.FIELDS:
@@ -163,7 +168,7 @@ def main():
                 ious.append(iou)
                 if worst is None or iou < worst[0]:
                     worst = (iou, i, f, int((m[f] != refs[i][1][f]).sum()), int(refs[i][1][f].sum()))
-        print(f"{pn:18s} IoU min {min(ious):.5f} mean {np.mean(ious):.5f}  max|dlogit| {max(errs):.3e}  "
+        print(f"{pn + ' head ' + hd:24s} IoU min {min(ious):.5f} mean {np.mean(ious):.5f}  max|dlogit| {max(errs):.3e}  "
               f"worst (iou, image, field, diff px, ref px) {worst}", flush=True)
 
 
