@@ -257,26 +257,56 @@ __device__ __forceinline__ float xsum_lane32(float x) {   // x[l] + x[l ^ 32]
 // dword per (class, row): the wave's TP = 4 pixel groups are one row pair x 32 columns, so each
 // class's ballots assemble into two 32-bit row words in scalar registers.  Same arithmetic per
 // logit (fmaf order, swaps, + bias), so bitwise the same logits and masks.
-template <int TP, int TW, int BACC>
+//
+// HT = _Float16 / __bf16 (the 16-bit plans, round 3): the 1x1 dot runs on two v_mfma_f32_16x16x32
+// per 16-pixel group instead of 48 FMAs + 6 swaps per lane: A = the head weights (16 rows = classes,
+// rows >= ncls zero), B = the ReLU outputs rounded to HT, fp32 accumulation, the bias added in fp32.
+// A lane's 16 channels (16q + 4t + e) are B's K slots 8q + j of MFMA h = t / 2 (v[8h + j]), so A's
+// K slot 8kq + j of MFMA h is channel 16kq + 8h + j; the logit of class c < 4 lands in lane (pixel,
+// q = 0) element c -- the lanes the stores and ballots below read.  Rounding the head's operands to
+// fp16 leaves the bench pages' masks unchanged (tools/numerics_emulate.py --head fp16: IoU min
+// 0.99945 either way); HT = float (the fp32 plan) keeps the exact fp32 FMA chains.
+template <int TP, int TW, int BACC, typename HT = float>
 __device__ __forceinline__ void head_epilogue(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0, int ox0,
                                               int g0, const float (&bv)[16], const float* head_w,
                                               const float* head_b) {
+  constexpr bool MH = sizeof(HT) == 2;
+  static_assert(!MH || kMaxClasses <= 4, "MFMA head: the classes are the 4 rows of lane group q = 0");
   const int H = a.H, W = a.W;
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4;
   const int col = lane & 15;
   const int ncls = a.ncls;
-  float hw[kMaxClasses][16], hb[kMaxClasses], cut[kMaxClasses];
+  float hw[MH ? 1 : kMaxClasses][16], hb[kMaxClasses], cut[kMaxClasses];
+  uint4 haf[2];   // MH: the A fragments (row = class col, K group q) of the two MFMAs
 #pragma unroll
   for (int c = 0; c < kMaxClasses; ++c) {
     const bool live = c < ncls;   // wave-uniform
     hb[c] = live ? head_b[c] : 0.f;
     cut[c] = a.thr_logit[c];
+    if constexpr (!MH) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x4 w4 = live ? *reinterpret_cast<const f32x4*>(head_w + c * 64 + q * 16 + 4 * i)
-                            : f32x4{0.f, 0.f, 0.f, 0.f};
-      hw[c][4 * i] = w4[0]; hw[c][4 * i + 1] = w4[1]; hw[c][4 * i + 2] = w4[2]; hw[c][4 * i + 3] = w4[3];
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 w4 = live ? *reinterpret_cast<const f32x4*>(head_w + c * 64 + q * 16 + 4 * i)
+                              : f32x4{0.f, 0.f, 0.f, 0.f};
+        hw[c][4 * i] = w4[0]; hw[c][4 * i + 1] = w4[1]; hw[c][4 * i + 2] = w4[2]; hw[c][4 * i + 3] = w4[3];
+      }
+    }
+  }
+  if constexpr (MH) {
+    typedef HT h8 __attribute__((ext_vector_type(8)));
+    const bool live = col < ncls;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      h8 w;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const f32x4 w4 = live ? *reinterpret_cast<const f32x4*>(head_w + col * 64 + 16 * q + 8 * h + 4 * i)
+                              : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[4 * i + e] = (HT)w4[e];
+      }
+      haf[h] = __builtin_bit_cast(uint4, w);
     }
   }
   auto logits_of = [&](int p, float (&logit)[kMaxClasses]) {
@@ -285,16 +315,30 @@ __device__ __forceinline__ void head_epilogue(const IgemmArgs& a, const f32x4 (&
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[t * 4 + e] = relu_nan(BACC ? acc[t][p][e] : acc[t][p][e] + bv[t * 4 + e]);
+    if constexpr (MH) {
+      typedef HT h8 __attribute__((ext_vector_type(8)));
+      f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < kMaxClasses; ++c) {
-      float sum = 0.f;
-      if (c < ncls) {   // wave-uniform: a dead class costs a scalar branch, not 16 FMAs + 2 swaps
+      for (int h = 0; h < 2; ++h) {
+        h8 b;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) sum = fmaf(hw[c][e], v[e], sum);
-        sum = xsum_lane16(sum);
-        sum = xsum_lane32(sum);
+        for (int j = 0; j < 8; ++j) b[j] = (HT)v[8 * h + j];
+        mfma_frag<HT>(d, haf[h], __builtin_bit_cast(uint4, b));
       }
-      logit[c] = sum + hb[c];
+#pragma unroll
+      for (int c = 0; c < kMaxClasses; ++c) logit[c] = d[c] + hb[c];   // valid in lanes q = 0
+    } else {
+#pragma unroll
+      for (int c = 0; c < kMaxClasses; ++c) {
+        float sum = 0.f;
+        if (c < ncls) {   // wave-uniform: a dead class costs a scalar branch, not 16 FMAs + 2 swaps
+#pragma unroll
+          for (int e = 0; e < 16; ++e) sum = fmaf(hw[c][e], v[e], sum);
+          sum = xsum_lane16(sum);
+          sum = xsum_lane32(sum);
+        }
+        logit[c] = sum + hb[c];
+      }
     }
   };
   auto pixel = [&](int p, int& oy, int& ox) {
@@ -380,7 +424,7 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
     bv[4 * i] = b4[0]; bv[4 * i + 1] = b4[1]; bv[4 * i + 2] = b4[2]; bv[4 * i + 3] = b4[3];
   }
   if constexpr (EPI == EPI_HEAD && !NOSTORE) {
-    head_epilogue<TP, TW, BACC>(a, acc, n, oy0, ox0, g0, bv, head_w, head_b);
+    head_epilogue<TP, TW, BACC, TO>(a, acc, n, oy0, ox0, g0, bv, head_w, head_b);
     return;
   }
 
