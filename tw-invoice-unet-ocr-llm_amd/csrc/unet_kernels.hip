@@ -204,6 +204,26 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
       : "v"(src), "s"(lds_addr));
 }
 
+// The same with the LDS destination given as a wave-uniform 32-bit LDS address (an SGPR value:
+// the LDS array's base + offsets built from scalars).  glds16 derives it from a generic pointer
+// per call -- a 64-bit VALU add, two v_readfirstlane and the generic -> LDS null check in front of
+// every DMA; the 8-wave and ConvTranspose rings issue 4-6 DMAs per wave and step (round 3).
+__device__ __forceinline__ void glds16_s(const void* src, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_addr)));
+}
+// LDS address of a __shared__ object (a constant for the kernel's one LDS array)
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_t)p));
+}
+
 // Pixel p (0..BP-1) of a block tile -> (row, col) inside the TH x 16 tile.  Pixels come
 // in groups of 16 = 2 rows x 8 columns, so an MFMA column group (lane & 15) covers whole
 // 2x2 pooling windows: partners are lanes ^1 and ^8.
@@ -1423,7 +1443,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   float* headb_s = headw_s + kMaxClasses * 64;
 
   const int tid = threadIdx.x;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar: the DMA addresses stay in SGPRs
+  const uint32_t lds0 = lds_addr_of(lds);
   const int lane = tid & 63;
   const int wp = wave;   // all 8 waves split the pixels; each covers all BR rows
 
@@ -1448,6 +1469,23 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   const int hseq_end = items * nch;
   // weight DMA pieces of this wave per step: pieces wave, wave + 8, ... of the step's PIECES
   const int wcnt = (PIECES - wave + NW - 1) / NW;
+  // The loop's counted wait: young * wcnt (+ HI when a halo issued after W(g+1) may stay in flight).
+  // young = NS - 2 on every step but the last ones, and wcnt is the same on every wave when PIECES
+  // % NW == 0, so the common waits are two immediates; the runtime switch (a compare chain with a
+  // barrier copy per case, ~40 scalar instructions and several branches per step) stays for the
+  // ring's last steps only (round 3).
+  constexpr int WCC = PIECES % NW == 0 ? PIECES / NW : -1;
+  auto loop_wait = [&](int young, bool hy) {
+    if constexpr (NS == 2 || WCC >= 0) {
+      if (young == NS - 2) {
+        constexpr int base = NS == 2 ? 0 : (NS - 2) * WCC;
+        if (hy) wait_vm_barrier<base + HI>();
+        else wait_vm_barrier<base>();
+        return;
+      }
+    }
+    wait_vm_barrier_rt(young * wcnt + (hy ? HI : 0));
+  };
 
   // weights of row tile ct in step order (the 4-wave ring's packing): piece j of a step = rows
   // 16j .. 16j+15; per lane one 16-byte chunk of row 16j + lane/4 at position chunk ^ ((row>>1)&3)
@@ -1482,20 +1520,20 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         hsrc[j] = ok ? in + pix * a.ldi * (long long)sizeof(T) + chk : zero + chk;
       }
     }
-    char* dst = lds + (hq_seq & 1) * HALO_BYTES + wave * HI * 1024;
+    const uint32_t dst = lds0 + (hq_seq & 1) * HALO_BYTES + wave * HI * 1024;
 #pragma unroll
-    for (int j = 0; j < HI; ++j) glds16(hsrc[j] + hq_c * 64, dst + j * 1024);
+    for (int j = 0; j < HI; ++j) glds16_s(hsrc[j] + hq_c * 64, dst + j * 1024);
     ++hq_seq;
     if (++hq_c == nch) { hq_c = 0; ++hq_i; }
   };
   // weights of step s into LDS slot `dst_slot` (this wave's pieces)
   auto issue_w_step = [&](int s, int dst_slot) {
     const char* src = wblk + (size_t)s * SLOT;
-    char* dst = lds + WOFF + dst_slot * SLOT;
+    const uint32_t dst = lds0 + WOFF + dst_slot * SLOT;
 #pragma unroll
     for (int k = 0; k < (PIECES + NW - 1) / NW; ++k) {
       const int j = wave + k * NW;
-      if (j < PIECES) glds16(src + j * 1024, dst + j * 1024);   // wave-uniform
+      if (j < PIECES) glds16_s(src + j * 1024, dst + j * 1024);   // wave-uniform
     }
   };
   int wq_s = 0, wq_slot = 0;
@@ -1544,7 +1582,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
         const char* src = ok ? reinterpret_cast<const char*>(a.x0) + ((long long)(n * H + iy) * W + ix) * 4 * sizeof(T)
                              : zero;
-        glds16(src, lds + G::XS_OFF + (i & 1) * G::XS1 + wave * 1024);
+        glds16_s(src, lds0 + G::XS_OFF + (i & 1) * G::XS1 + wave * 1024);
       }
     }
   };
@@ -1868,7 +1906,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
       const bool hyoung = tap < NS - 1 && tap < SPC - 1 && hseq + 1 < hseq_end;
       if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }   // see ring_body
-      else wait_vm_barrier_rt(young * wcnt + (hyoung ? HI : 0));
+      else loop_wait(young, hyoung);
     }
     bool tile_end = false;
     if (++tap == SPC) {
@@ -1891,7 +1929,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         int young = total - 2 - g;
         young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
         if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }
-        else wait_vm_barrier_rt(young * wcnt);   // the last halo issue is older than W(g+1)
+        else loop_wait(young, false);   // the last halo issue is older than W(g+1)
         // no vmcnt(0) drain: the stores retire under the next step's wait (see ring_body)
         conv_epilogue<TO, TO, TP, EPI_UPSCATTER, TW, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[0]), n,
                                                            ty * 16, tx * TW, wp * TP, 64 * quad, nullptr, nullptr,
@@ -1974,7 +2012,8 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
   // order) drained every DMA in flight and the previous pixel groups' scatter stores per tile
   __shared__ __attribute__((aligned(16))) float bias_s[BR];
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const uint32_t lds0 = lds_addr_of(lds);
   const int wr = wave >> 2, wp = wave & 3;   // row group (WRW = 2), pixel group
   int bid;
   {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one walker
@@ -2005,10 +2044,10 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
   };
   auto issue = [&](int g) {
     const int i = g / S, c = g - (g / S) * S;
-    char* As = lds + (g % NS) * SLOT;
+    const uint32_t As = lds0 + (g % NS) * SLOT;
 #pragma unroll
     for (int j = 0; j < WI; ++j)
-      glds16(wblk + ((size_t)ct * S + c) * ASLOT + j * 1024, As + (wave * WI + j) * 1024);
+      glds16_s(wblk + ((size_t)ct * S + c) * ASLOT + j * 1024, As + (wave * WI + j) * 1024);
     int n, ty, tx;
     tile_of(i, n, ty, tx);
 #pragma unroll
@@ -2019,7 +2058,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
       const bool ok = iy < H && ix < W;
       const char* src = ok ? in + (((long long)(n * H + iy) * W + ix) * a.ldi + (long long)c * BKE) * (long long)sizeof(T) + chk
                            : zero + chk;
-      glds16(src, As + ASLOT + (wave * BI + j) * 1024);
+      glds16_s(src, As + ASLOT + (wave * BI + j) * 1024);
     }
   };
 
