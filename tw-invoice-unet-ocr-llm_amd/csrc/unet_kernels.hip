@@ -1533,7 +1533,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 #pragma unroll
     for (int k = 0; k < (PIECES + NW - 1) / NW; ++k) {
       const int j = wave + k * NW;
-      if (j < PIECES) glds16_s(src + j * 1024, dst + j * 1024);   // wave-uniform
+      // wave-uniform; no test at all when every wave has the same count (straight-line issue: the
+      // compiler had moved the tested pieces out of line, a taken branch each)
+      if (PIECES % NW == 0 || j < PIECES) glds16_s(src + j * 1024, dst + j * 1024);
     }
   };
   int wq_s = 0, wq_slot = 0;
@@ -2042,24 +2044,34 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
     ty = mt % a.tiles_y;
     n = mt / a.tiles_y;
   };
-  auto issue = [&](int g) {
-    const int i = g / S, c = g - (g / S) * S;
-    const uint32_t As = lds0 + (g % NS) * SLOT;
+  // Steps are issued strictly in order, so the issue side keeps cursors instead of dividing g by S
+  // and re-deriving the tile per step (two scalar divisions and 64-bit VALU address math per piece,
+  // round 3): at a tile's first step the B pieces' per-lane pointers are set once (the zero page for
+  // pixels outside the image -- 4 KB, so + c * 64 stays inside it), every step adds c * 64.
+  int iss_c = 0, iss_i = 0, iss_slot = 0;
+  const char* bsrc[BI];
+  const char* wct = wblk + (size_t)ct * S * ASLOT;
+  auto issue = [&]() {
+    const uint32_t As = lds0 + iss_slot * SLOT;
 #pragma unroll
     for (int j = 0; j < WI; ++j)
-      glds16_s(wblk + ((size_t)ct * S + c) * ASLOT + j * 1024, As + (wave * WI + j) * 1024);
-    int n, ty, tx;
-    tile_of(i, n, ty, tx);
+      glds16_s(wct + (size_t)iss_c * ASLOT + j * 1024, As + (wave * WI + j) * 1024);
+    if (iss_c == 0) {
+      int n, ty, tx;
+      tile_of(iss_i, n, ty, tx);
 #pragma unroll
-    for (int j = 0; j < BI; ++j) {
-      const int r = (wave * BI + j) * 16 + (lane >> 2), py = r >> 4, px = r & 15;
-      const int iy = ty * 16 + py, ix = tx * 16 + px;
-      const int chk = ((lane & 3) ^ ((py & 1) << 1)) << 4;
-      const bool ok = iy < H && ix < W;
-      const char* src = ok ? in + (((long long)(n * H + iy) * W + ix) * a.ldi + (long long)c * BKE) * (long long)sizeof(T) + chk
-                           : zero + chk;
-      glds16_s(src, As + ASLOT + (wave * BI + j) * 1024);
+      for (int j = 0; j < BI; ++j) {
+        const int r = (wave * BI + j) * 16 + (lane >> 2), py = r >> 4, px = r & 15;
+        const int iy = ty * 16 + py, ix = tx * 16 + px;
+        const int chk = ((lane & 3) ^ ((py & 1) << 1)) << 4;
+        const bool ok = iy < H && ix < W;
+        bsrc[j] = ok ? in + ((long long)(n * H + iy) * W + ix) * a.ldi * (long long)sizeof(T) + chk : zero + chk;
+      }
     }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) glds16_s(bsrc[j] + iss_c * BKE * (int)sizeof(T), As + ASLOT + (wave * BI + j) * 1024);
+    if (++iss_slot == NS) iss_slot = 0;
+    if (++iss_c == S) { iss_c = 0; ++iss_i; }
   };
 
   // Every tile's accumulators start at the ConvTranspose bias (rows wr*16*TC + 64h + 16q + 4t + e of
@@ -2086,7 +2098,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
 
 #pragma unroll
   for (int k = 0; k < NS - 1; ++k)
-    if (k < total) issue(k);
+    if (k < total) issue();
   for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];   // (the wait below covers it)
   {   // step 0 landed; steps 1 .. NS-2 may stay in flight
     const int young = total - 1 < NS - 2 ? total - 1 : NS - 2;
@@ -2096,7 +2108,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
 
   int c = 0, item = 0, wskip = 0;
   for (int g = 0; g < total; ++g) {
-    if (g + NS - 1 < total) issue(g + NS - 1);
+    if (g + NS - 1 < total) issue();
     const char* As = lds + (g % NS) * SLOT + wrow;
     const char* Bs = lds + (g % NS) * SLOT + ASLOT;
     frag_t bq[TP], ar[3];
