@@ -1573,10 +1573,13 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 
   // ---- HS: fused first conv (down1.0) -> halo chunks (see ring_body) ----
   // window DMA of tile i: thread L < 360 copies input pixels (2*(L%18), +1) of window row L/18
-  auto issue_xs = [&](int i) {   // -> window buffer i & 1
+  // (HS) the tile coordinates of the current and the next tile are derived once per tile (tile_of
+  // is two scalar divisions) and handed to the window DMA and the halo computation
+  struct TileXY { int n, ty, tx; };
+  auto tile_xy = [&](int i) { TileXY t; tile_of(i, t.n, t.ty, t.tx); return t; };
+  auto issue_xs = [&](int i, const TileXY& tc) {   // -> window buffer i & 1
     if constexpr (HS != 0) {
-      int n, ty, tx;
-      tile_of(i, n, ty, tx);
+      const int n = tc.n, ty = tc.ty, tx = tc.tx;
       const int L = tid;
       if (L < 20 * (G::XW / 2)) {   // lanes past the window stay inactive (no LDS write)
         const int yy = L / (G::XW / 2), seg = L - (L / (G::XW / 2)) * (G::XW / 2);
@@ -1624,11 +1627,10 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   static_assert(HS == 0 || (HWD == 34 && HGR == 39), "computed halo groups: 9 row pairs x 4 + 3");
   // cb (the 32-channel chunk: selects w0f / b0v) and part are compile-time (std::integral_constant):
   // with runtime values the two register arrays are indexed dynamically and go to scratch.
-  auto compute_halo = [&](int i, auto cbc, int hb, auto partc) {
+  auto compute_halo = [&](int i, const TileXY& tc, auto cbc, int hb, auto partc) {
     constexpr int cb = decltype(cbc)::value, part = decltype(partc)::value;
     if constexpr (HS != 0) {
-      int n, ty, tx;
-      tile_of(i, n, ty, tx);
+      const int ty = tc.ty, tx = tc.tx;
       const char* xs = lds + G::XS_OFF + (i & 1) * G::XS1;
       char* dst = lds + hb * HALO_BYTES;
       const int qq = lane >> 4, c = lane & 15;
@@ -1690,10 +1692,11 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   using C0 = std::integral_constant<int, 0>;
   using C1 = std::integral_constant<int, 1>;
   if constexpr (HS != 0) {
-    issue_xs(0);
+    const TileXY t0 = tile_xy(0);
+    issue_xs(0, t0);
     wait_vm_barrier<0>();
-    compute_halo(0, C0{}, 0, C0{});
-    compute_halo(0, C0{}, 0, C1{});
+    compute_halo(0, t0, C0{}, 0, C0{});
+    compute_halo(0, t0, C0{}, 0, C1{});
   } else {
     issue_halo();
   }
@@ -1772,26 +1775,28 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       }
       mfma_taps<T, TC, TP, 9>(acc, hs9, ws9, prow);
     };
-    auto halo_all = [&](int i, auto cbc) {   // both halves of chunk cb of tile i -> buffer cb
-      compute_halo(i, cbc, decltype(cbc)::value, C0{});
-      compute_halo(i, cbc, decltype(cbc)::value, C1{});
+    auto halo_all = [&](int i, const TileXY& tc, auto cbc) {   // both halves of chunk cb of tile i -> buffer cb
+      compute_halo(i, tc, cbc, decltype(cbc)::value, C0{});
+      compute_halo(i, tc, cbc, decltype(cbc)::value, C1{});
     };
+    TileXY cur = tile_xy(0);
     for (int item = 0; item < items; ++item) {
       const bool more = item + 1 < items;
-      if (more) issue_xs(item + 1);
+      const TileXY nxt = more ? tile_xy(item + 1) : cur;
+      if (more) issue_xs(item + 1, nxt);
       taps9(0);
-      halo_all(item, C1{});
+      halo_all(item, cur, C1{});
       wait_vm_barrier<0>();
       taps9(1);
-      if (more) halo_all(item + 1, C0{});
+      if (more) halo_all(item + 1, nxt, C0{});
       wait_vm_barrier<63>();   // barrier only: no load is waited for here
-      int n, ty, tx;
-      tile_of(item, n, ty, tx);
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<TO, TQ, TP, EPI, TW, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
-                                                 tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s, headb_s);
+        conv_epilogue<TO, TQ, TP, EPI, TW, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), cur.n,
+                                                 cur.ty * 16, cur.tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h,
+                                                 headw_s, headb_s);
       init_acc_bias(0, TC);
+      cur = nxt;
     }
     return;
   }
