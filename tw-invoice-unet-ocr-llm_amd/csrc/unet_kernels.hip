@@ -549,9 +549,12 @@ __device__ __forceinline__ void wait_vm_barrier() {
 // right after a barrier of the 8-wave ring, whose two waves per SIMD belong to ONE block.
 // hs[k]: halo fragment base of tap k (+ prow[p] per pixel group), ws[k]: weight row base of tap
 // k (+ t * 1 KB per 16-row group).  Same MFMA sequence per accumulator as one tap at a time.
-template <typename T, int TC, int TP, int NT>
+// mid (optional): work issued after the first tap's MFMAs -- the step's LDS-DMA issue, which then
+// runs while those MFMAs execute instead of in front of the step's first fragment reads (round 3).
+struct NoMid { __device__ void operator()() const {} };
+template <typename T, int TC, int TP, int NT, typename Mid = NoMid>
 __device__ __forceinline__ void mfma_taps(f32x4 (&acc)[TC][TP], const char* const (&hs)[NT],
-                                          const char* const (&ws)[NT], const int (&prow)[TP]) {
+                                          const char* const (&ws)[NT], const int (&prow)[TP], Mid mid = Mid{}) {
   constexpr int NR = TC + TP, NM = TC * TP;
   static_assert(NM % NR == 0, "read / MFMA interleave");
   frag_t fa[2][TC], fb[2][TP];
@@ -581,6 +584,7 @@ __device__ __forceinline__ void mfma_taps(f32x4 (&acc)[TC][TP], const char* cons
     } else {
       __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
     }
+    if (k == 0) mid();   // after the first tap's MFMAs (and the next tap's reads) are issued
   }
 }
 
@@ -588,9 +592,9 @@ __device__ __forceinline__ void mfma_taps(f32x4 (&acc)[TC][TP], const char* cons
 // double-buffered): the A fragments of all NT taps form ONE stream through a 3-register ring two
 // row groups ahead (crossing tap boundaries), and only the TP B fragments are double-buffered --
 // tap k+1's are read under the first TP row groups of tap k.
-template <typename T, int TC, int TP, int NT>
+template <typename T, int TC, int TP, int NT, typename Mid = NoMid>
 __device__ __forceinline__ void mfma_taps_astream(f32x4 (&acc)[TC][TP], const char* const (&hs)[NT],
-                                                  const char* const (&ws)[NT], const int (&prow)[TP]) {
+                                                  const char* const (&ws)[NT], const int (&prow)[TP], Mid mid = Mid{}) {
   static_assert(TC >= TP && TC >= 3, "B prefetch spread over the row groups");
   frag_t ar[3], fb[2][TP];
   auto lda = [&](int j) { return *reinterpret_cast<const frag_t*>(ws[j / TC] + (j % TC) * 16 * 64); };
@@ -613,6 +617,7 @@ __device__ __forceinline__ void mfma_taps_astream(f32x4 (&acc)[TC][TP], const ch
       if (j + 2 < NT * TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       if (k + 1 < NT && t < TP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+      if (j == 1) mid();   // after the first two row groups' MFMAs
     }
   }
 }
@@ -1856,8 +1861,16 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     // the next chunk's halo is issued AFTER this step's weights: vmcnt retires in issue order, so
     // the halo then stays in flight through the wait for W(g+2) too (NS - 1 steps of latency
     // instead of NS - 2; it is needed only at the chunk end)
-    if (!WST && g + NS - 1 < total) issue_w();
-    if (HS == 0 && hnext) issue_halo();
+    // this step's LDS-DMA (W(g+NS-1), then the next chunk's halo): issued from inside the tap
+    // sequence, after its first MFMAs (mfma_taps* `mid`); the step paths without a hook issue it here
+    const bool dma_w = !WST && g + NS - 1 < total, dma_h = HS == 0 && hnext;
+    auto dma = [&]() {
+      if (dma_w) issue_w();
+      if (dma_h) issue_halo();
+    };
+    // (TPS = 9, conv1.0's two-slot ring: the next step's DMA has one step of cover only, so it is
+    // issued first, as before: from inside the taps it measured +0.8 %, profiles/tune_r3z_*)
+    if constexpr (!((WST && HS == 0 && TPS == 3 && TC * TP % (TC + TP) == 0) || TPS == 3)) dma();
     if constexpr (WST && HS == 0 && TPS == 3 && TC * TP % (TC + TP) == 0) {
       // weight-stationary, DMA'd halo: no barrier inside a chunk, so its nine taps (three steps)
       // run as one pipelined sequence at the chunk's first step; the other two only keep count
@@ -1871,7 +1884,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
           hs9[k] = lds + (hseq & 1) * HALO_BYTES + (dy * HWD + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
           ws9[k] = wrow + (ws0 + dy) * SLOT + dx * WSLOT;
         }
-        mfma_taps<T, TC, TP, 9>(acc, hs9, ws9, prow);
+        mfma_taps<T, TC, TP, 9>(acc, hs9, ws9, prow, dma);
+      } else {
+        dma();
       }
     } else if constexpr (TPS == 9) {
       // one step = a whole 32-channel chunk (nine taps, one barrier): the weights of the next chunk
@@ -1894,8 +1909,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         hs3[t] = lds + (hseq & 1) * HALO_BYTES + (tap * HWD + t) * 64 + ((q ^ ((px_lane + t) & 3)) << 4);
         ws3[t] = wrow + wslot * SLOT + t * WSLOT;
       }
-      if constexpr (TC * TP % (TC + TP) == 0) mfma_taps<T, TC, TP, 3>(acc, hs3, ws3, prow);
-      else mfma_taps_astream<T, TC, TP, 3>(acc, hs3, ws3, prow);
+      if constexpr (TC * TP % (TC + TP) == 0) mfma_taps<T, TC, TP, 3>(acc, hs3, ws3, prow, dma);
+      else mfma_taps_astream<T, TC, TP, 3>(acc, hs3, ws3, prow, dma);
     } else {
 #pragma unroll
       for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
@@ -2113,7 +2128,9 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
 
   int c = 0, item = 0, wskip = 0;
   for (int g = 0; g < total; ++g) {
-    if (g + NS - 1 < total) issue();
+    // this step's LDS-DMA (step g+NS-1, into the slot step g-1 released) is issued after the first two
+    // row groups' MFMAs, so it runs while they execute (as in the 8-wave ring, round 3)
+    const bool dma = g + NS - 1 < total;
     const char* As = lds + (g % NS) * SLOT + wrow;
     const char* Bs = lds + (g % NS) * SLOT + ASLOT;
     frag_t bq[TP], ar[3];
@@ -2131,6 +2148,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
         mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
       if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+      if (t == 1 && dma) issue();
     }
     // step g+1 must have landed; step g+2 (issued above) may stay in flight
     {   // step g+1 landed; steps g+2 .. g+NS-1 (issued) may stay in flight
