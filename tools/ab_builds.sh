@@ -19,6 +19,7 @@ for b in $BUILDS; do
   fi
   echo "ab $b ok"
 done
+rm -f gpurun_out/${TAG}_*.npz   # only the bitwise comparison reads them (and 4 builds' logits exceed gpurun's 64 MiB pull)
 for i in 1 2; do
   for b in $BUILDS; do
     UNET_MI355X_LIB=$(lib $b) timeout -k 10 300 python tools/tune.py --dtype mixed --batch 256 --reps 3 > gpurun_out/${TAG}_tune_$b$i.txt 2>&1
