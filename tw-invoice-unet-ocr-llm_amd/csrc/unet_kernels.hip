@@ -1834,7 +1834,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       init_up_bias(0);
     }
   };
-  auto stepT = [&](int g) {   // one quadrant: acc[t] += A(kb, t) x xb[kb], kb = 0..3 (the ring's K order)
+  auto stepT = [&](int g, bool dma) {   // one quadrant: acc[t] += A(kb, t) x xb[kb], kb = 0..3 (the ring's K order)
     if constexpr (UPF) {
       const char* Ws = wrow + (g % NS) * SLOT;
       frag_t ar[3];
@@ -1850,6 +1850,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
           mfma_frag<T>(acc[j & 3][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, xb[p][j >> 2]));
         if (j + 2 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+        if (j == 1 && dma) issue_w();   // the step's weight DMA under the first MFMAs (as the conv steps)
       }
     }
   };
@@ -1946,8 +1947,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 #pragma nounroll
       for (int quad = 0; quad < SU; ++quad) {
         ++g;
-        if (g + NS - 1 < total) issue_w();
-        stepT(g);
+        stepT(g, g + NS - 1 < total);
         int young = total - 2 - g;
         young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
         if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }
