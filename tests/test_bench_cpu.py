@@ -106,3 +106,14 @@ def test_launch_table_credits_each_kernel_with_its_own_work():
     x2 = n * (s // 2) ** 2 * 128 * e
     assert rows[18][3] == (bench.launch_bytes(bench.LAUNCHES[18], n, s, s, c, e) +
                            bench.launch_bytes(bench.LAUNCHES[19], n, s, s, c, e) - 2 * x2)
+
+
+def test_pmc_summary_labels_mangled_and_demangled_names():
+    """rocprofv3 demangles some kernel names (the fp32 kernels) and leaves the 16-bit ones mangled:
+    both must map to bench.py's kernel labels, or the roofline's traffic comes out as 0."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from pmc_summary import label_of
+    assert label_of("void unet::conv3x3_halo_kernel<float, 1, 4, 8, 2, 3, 0>(unet::IgemmArgs)") == \
+        "conv3x3_halo_kernel<float, 1, 4, 8, 2, 3, 0>"
+    assert label_of("_ZN4unet20conv3x3_ring8_kernelIDF16bLi8ELi3ELi0ELi3ELi0EDF16bDF16bLi0ELi0EEEvNS_9IgemmArgsE") == \
+        "conv3x3_ring8_kernel<__bf16, 8, 3, 0, 3, 0, __bf16, __bf16, 0, 0>"

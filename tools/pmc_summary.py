@@ -27,6 +27,9 @@ TYPES = {"f": "float", "DF16b": "__bf16", "DF16_": "_Float16"}
 def label_of(name):
     """Our mangled kernel symbol -> "kernel<args>" (bench.py / unet_launch_label spelling):
     template arguments are element types (DF16b, DF16_, f) or ints (Li<n>E)."""
+    d = re.match(r"(?:void )?unet::(\w+<[^()]*>)\(", name)   # rocprofv3 demangles some names (the fp32 kernels)
+    if d:
+        return d.group(1)
     m = re.match(r"_ZN4unet(\d+)(\w+)", name)
     if not m:
         return name
@@ -79,7 +82,7 @@ def main():
         rows = load_pass(p)
         # the forward's own launches: every unet:: kernel except the pre/post-processing ones
         ours = [(did, v) for did, v in sorted(rows.items())
-                if v[0].startswith("_ZN4unet") and not any(s in v[0] for s in ("mask_boxes", "resample", "nhwc_to_nchw",
+                if v[0].startswith(("_ZN4unet", "void unet::", "unet::")) and not any(s in v[0] for s in ("mask_boxes", "resample", "nhwc_to_nchw",
                                                                                 "to_planar", "x_to_nchw"))]
         last = ours[-len(launches):]
         for i, (did, (name, ctr)) in enumerate(last):
