@@ -463,7 +463,23 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
         if (EPI != EPI_UPSCATTER) x = relu_nan(x);
         v[t * 4 + e] = x;
       }
-    if constexpr (NOSTORE) {   // ablation builds: the epilogue arithmetic without its stores
+    if constexpr (NOSTORE == 2 && sizeof(TO) == 2 && (EPI == EPI_STORE || EPI == EPI_POOL)) {
+      // ablation builds: the stores alone (zeros to the same addresses, no arithmetic)
+      if (inside) {
+        TO* d = reinterpret_cast<TO*>(a.out) + ((long long)(n * H + oy) * W + ox) * a.ldo + a.out_off + row0 +
+                swz_store_off(q);
+        *reinterpret_cast<uint4*>(d) = uint4{0u, 0u, 0u, 0u};
+        *reinterpret_cast<uint4*>(d + 32) = uint4{0u, 0u, 0u, 0u};
+      }
+      if constexpr (EPI == EPI_POOL) {
+        if ((col & 9) == 0 && oy + 1 < H && ox + 1 < W) {
+          TQ* d = reinterpret_cast<TQ*>(a.out2) + ((long long)(n * (H >> 1) + (oy >> 1)) * (W >> 1) + (ox >> 1)) * a.ldo2 +
+                  row0 + swz_store_off(q);
+          *reinterpret_cast<uint4*>(d) = uint4{0u, 0u, 0u, 0u};
+          *reinterpret_cast<uint4*>(d + 32) = uint4{0u, 0u, 0u, 0u};
+        }
+      }
+    } else if constexpr (NOSTORE) {   // ablation builds: the epilogue arithmetic without its stores
 #pragma unroll
       for (int e = 0; e < 16; ++e) asm volatile("" ::"v"(v[e]));
       if constexpr (EPI == EPI_POOL) {
@@ -1422,7 +1438,8 @@ __device__ __forceinline__ void wait_vm_barrier_rt(int n) {
 // 20 x 36 window of the pre-cast input on 16x16x16 MFMAs); needs WST (the loop then has a barrier
 // after every step: the window is re-filled while the halo of the next tile is computed from it).
 // ABL (timing-only ablation builds, `make abl`): 5 = no tile epilogue (the accumulators are kept
-// alive, nothing is stored) -- the per-tile epilogue's share of a layer, wrong outputs by construction.
+// alive, nothing is stored) -- the per-tile epilogue's share of a layer, wrong outputs by construction;
+// 6 = the epilogue's arithmetic without its stores; 7 = its stores (zeros) without the arithmetic.
 template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a) {
   using G = Ring8Geom<T, TCW, NS, TPS, WST, HS>;
@@ -1976,6 +1993,15 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
           for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int p = 0; p < TP; ++p) asm volatile("" ::"v"(acc[4 * h + t][p]));
+        } else if constexpr (ABL == 6 || ABL == 7) {   // 6: arithmetic without stores; 7: stores without arithmetic
+          if constexpr (ABL == 7)   // the accumulators stay alive (else the MFMAs are dead code)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+              for (int p = 0; p < TP; ++p) asm volatile("" ::"v"(acc[4 * h + t][p]));
+          conv_epilogue<TO, TQ, TP, EPI, TW, ABL == 6 ? 1 : 2, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n,
+                                                               ty * 16, tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h,
+                                                               headw_s, headb_s);
         } else {
           conv_epilogue<TO, TQ, TP, EPI, TW, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
                                                    tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s,
@@ -2375,9 +2401,11 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ, ABL>(a, s);
         break;
       case CFG_RING8_R128:
-        if constexpr (ABL == 5 && EPI != EPI_HEAD) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ, 0, 5>(a, s);
+        if constexpr (ABL >= 5 && ABL <= 7 && EPI != EPI_HEAD) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ, 0, ABL>(a, s);
         break;
-      case CFG_RING8_R64_T9: if constexpr (ABL == 5) return launch_ring8<T, 4, 2, EPI, 9, 0, TO, TQ, 0, 5>(a, s); break;
+      case CFG_RING8_R64_T9:
+        if constexpr (ABL >= 5 && ABL <= 7 && EPI != EPI_HEAD) return launch_ring8<T, 4, 2, EPI, 9, 0, TO, TQ, 0, ABL>(a, s);
+        break;
       case CFG_RING8_R64_WS: if constexpr (ABL == 5) return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ, 0, 5>(a, s); break;
       default: break;
     }
@@ -2438,7 +2466,7 @@ static hipError_t launch_typed(int cfg, int taps, int epi, const IgemmArgs& a, h
     }
     switch (cfg / 16) {
       UNET_ABL_CASE(1) UNET_ABL_CASE(2) UNET_ABL_CASE(3) UNET_ABL_CASE(4) UNET_ABL_CASE(5) UNET_ABL_CASE(6)
-      UNET_ABL_CASE(8)
+      UNET_ABL_CASE(7) UNET_ABL_CASE(8)
       default: return hipErrorInvalidValue;
     }
 #undef UNET_ABL_CASE
