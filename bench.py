@@ -52,10 +52,12 @@ from unet_mi355x import synthetic as syn  # noqa: E402
 METRIC = "invoice masks/sec at 512x512 bs256, 1/2/4/8 MI355X; IoU vs CPU ref"
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "mixed": 2500.0, "fp32": 157.3}   # dense MFMA (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
+HEAD16 = ("1x1 head on 16-bit MFMA operands (conv1.3's ReLU outputs and the out_conv weights rounded to the "
+          "layer's type), fp32 accumulation and fp32 bias")
 PLAN = {"mixed": "bf16 storage at resolution levels 2-4 (64..1024 ch, 128^2..32^2), fp16 at levels 0-1 "
-                 "(512^2, 256^2); fp32 accumulation, fp32 head",
-        "bf16": "bf16 storage, fp32 accumulation, fp32 head", "fp16": "fp16 storage, fp32 accumulation, fp32 head",
-        "fp32": "fp32 (exact-fp32 MFMA)"}
+                 "(512^2, 256^2); fp32 accumulation; " + HEAD16,
+        "bf16": "bf16 storage, fp32 accumulation; " + HEAD16, "fp16": "fp16 storage, fp32 accumulation; " + HEAD16,
+        "fp32": "fp32 (exact-fp32 MFMA), fp32 head"}
 STRONG_GLOBAL = (256, 1024)   # north_star's batch 256 and BASELINE config 4's batch 1024
 
 # launch order of include/unet_mi355x.h: (name, cin, cout, input level, kind); the kernel
@@ -331,10 +333,12 @@ def make_leg(runner, rank, world, n_total, per_rank, seed, S, C, dev, chunk):
     segment = runner.segment_fn()
 
     def step():
+        if n_local <= chunk:     # the library's data-parallel step (tests/test_dist_cpu.py drives it too)
+            udist.sharded_mask_step(segment, x, gather)
+            return
         for i in range(0, n_local, chunk):
             segment(x[i:i + chunk], gather.local[i:i + chunk])
-        if world > 1:
-            gather()
+        gather()
     return {"x": x, "gather": gather, "step": step, "n_total": n_total, "n_local": n_local}
 
 
@@ -573,6 +577,8 @@ def main():
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-layer-profile", action="store_true")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling shapes (global 256 / 1024)")
+    ap.add_argument("--strong-global", type=int, nargs="+", default=None,
+                    help="global batches of the strong-scaling legs (default 256 1024 at 512x512; tests use small ones)")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 config-2 leg")
     ap.add_argument("--fp32-batch", type=int, default=32)
     ap.add_argument("--fp32-steps", type=int, default=5)
@@ -616,8 +622,9 @@ def main():
     S, C = args.size, args.channels
     strong = args.global_batch is not None
     legs_cfg = [("main", args.global_batch if strong else None, None if strong else args.batch)]
-    if not args.no_strong and S == 512:
-        legs_cfg += [(f"strong_{g}", g, None) for g in STRONG_GLOBAL if not (strong and g == args.global_batch)]
+    strong_global = args.strong_global or (STRONG_GLOBAL if S == 512 else ())
+    if not args.no_strong:
+        legs_cfg += [(f"strong_{g}", g, None) for g in strong_global if not (strong and g == args.global_batch)]
     chunk = max(args.batch, udist.shard_bounds(args.global_batch, 0, world)[1]) if strong else args.batch
     runner.reserve(chunk, S)
 
@@ -626,6 +633,7 @@ def main():
     B = main_leg["n_local"]
     if not args.standin and args.weights == "structured":
         runner.recentre(main_leg["x"])
+        runner.handle()   # re-pack now: the legs' step functions hold this handle and never re-check weights
     res = time_leg(main_leg, args.steps, args.warmup, sync, dev, per_step_events=not args.standin)
 
     # ---- strong-scaling shapes (same timing protocol, fewer steps)

@@ -1,7 +1,7 @@
 """Generate the golden fixtures by running the REFERENCE itself (survey container only).
 
 Usage (from the repo root, where /root/reference exists):
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--only-pretrained]
 
 It imports ``unet_model`` and ``inference`` from /root/reference (SURVEY.md §8c:
 importable, nothing denied), loads seeded synthetic weights (the real
@@ -59,9 +59,72 @@ def forward_with_hooks(model, x):
     return out, inter
 
 
+PRETRAINED_512_PAGES = (0, 13, 37, 63)    # indices into the bench's 64 unique pages (bench.gen_pages seed 1000)
+
+
+def quantised_pages(seed, n, size):
+    """Invoice pages as a photo would deliver them: uint8 gray (x255, round half up), replicated
+    x3.  x = u8 / 255 is then exactly what inference.preprocess produces for that photo."""
+    pages = syn.invoice_pages(seed, n, size, size, 1)[:, 0]
+    return (pages.astype(np.float64) * 255.0 + 0.5).astype(np.uint8)
+
+
+def pretrained_cases(ref_unet, ref_inf):
+    """The benchmarked shapes pinned to the reference: the trained-like
+    "pretrained" weight profile the bench's IoU claims use, on the bench's own pages.
+
+    * pretrained_512_pages.npz: 4 of the bench's 512x512 pages (uint8-quantised), masks from the
+      REFERENCE's run_unet (inference.py:50-79: load_model, resize, preprocess, forward, sigmoid,
+      per-field thresholds) as bit-packed arrays, its 1/8-subsampled logits, and the sha256 of
+      the network input preprocess() built.
+    * pretrained_1024_page.npz: one 1024x1024 page (BASELINE config 5 shape) through the
+      reference UNet.forward; masks with inference.py:72-79's sigmoid + thresholds applied to it.
+    """
+    import hashlib
+    from PIL import Image
+    sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
+    u8 = quantised_pages(1000, max(PRETRAINED_512_PAGES) + 1, 512)[list(PRETRAINED_512_PAGES)]
+    model = build(ref_unet, sd, 3, 3)
+    payload = dict(page_index=np.array(PRETRAINED_512_PAGES, np.int64), pages_u8=u8,
+                   sd_sha256=np.array(syn.state_dict_checksum(sd)), profile=np.array("pretrained"))
+    with tempfile.TemporaryDirectory() as td:
+        ck = os.path.join(td, "ckpt.pth")
+        torch.save(to_torch_sd(sd), ck)
+        ref_inf.DEVICE = "cpu"
+        for j, page in enumerate(u8):
+            pil = Image.fromarray(np.stack([page] * 3, axis=-1), mode="RGB")
+            masks, _ = ref_inf.run_unet(pil, ck)
+            x = ref_inf.preprocess(pil.resize((512, 512)))
+            assert np.array_equal(x.numpy()[0, 0], page.astype(np.float32) / 255.0)
+            with torch.no_grad():
+                logits = model(x)[0].numpy()
+            payload[f"x_sha256_{j}"] = np.array(hashlib.sha256(x.numpy().tobytes()).hexdigest())
+            payload[f"logits_sub8_{j}"] = logits[:, ::8, ::8].copy()
+            for k in ref_inf.FIELDS:
+                payload[f"maskbits_{k}_{j}"] = np.packbits(masks[k].astype(np.uint8), axis=-1, bitorder="little")
+            print("pretrained_512 page", PRETRAINED_512_PAGES[j], {k: round(float(masks[k].mean()), 4) for k in masks})
+    np.savez_compressed(os.path.join(HERE, "pretrained_512_pages.npz"), **payload)
+
+    page = quantised_pages(1000, 1, 1024)[0]
+    x = torch.from_numpy(np.ascontiguousarray(np.stack([page] * 3)[None].astype(np.float32) / 255.0))
+    with torch.no_grad():
+        logits = model(x)
+        prob = torch.sigmoid(logits.squeeze(0)).numpy()
+    thr = {"invoice_no": 0.25, "date": 0.40, "total_amount": 0.30}    # inference.py:76-78
+    payload = dict(page_u8=page, sd_sha256=np.array(syn.state_dict_checksum(sd)), profile=np.array("pretrained"),
+                   logits_sub8=logits[0].numpy()[:, ::8, ::8].copy())
+    for i, k in enumerate(ref_inf.FIELDS):
+        payload[f"maskbits_{k}"] = np.packbits((prob[i] > thr[k]).astype(np.uint8), axis=-1, bitorder="little")
+    np.savez_compressed(os.path.join(HERE, "pretrained_1024_page.npz"), **payload)
+    print("pretrained_1024", {k: round(float((prob[i] > thr[k]).mean()), 4) for i, k in enumerate(ref_inf.FIELDS)})
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref_unet, ref_inf = ref_modules()
+    if "--only-pretrained" in sys.argv:
+        pretrained_cases(ref_unet, ref_inf)
+        return
     cases = [
         # name, n_channels, H, W, N, profile, seed, input kind, keep intermediates
         ("unet_c3_h64w64_n2_structured", 3, 64, 64, 2, "structured", 1, "invoice", False),
@@ -124,6 +187,7 @@ def main():
         payload["crop_none_" + k] = np.bool_(cr is None)
     np.savez_compressed(os.path.join(HERE, "run_unet_600x400.npz"), **payload)
     print("run_unet_600x400", {k: (masks[k].mean(), None if crops[k] is None else crops[k].size) for k in masks})
+    pretrained_cases(ref_unet, ref_inf)
 
 
 if __name__ == "__main__":

@@ -57,6 +57,17 @@ def test_self_spawn_strong_scaling_ragged():
     assert out["config"]["global_batch"] == 10 and out["config"]["per_gpu_batch"] == 4   # 4 + 3 + 3
 
 
+def test_strong_legs_chunked_two_ranks():
+    """A strong-scaling leg whose shard is larger than the workspace chunk (global 10 over 2 ranks =
+    5 images per rank, chunk = --batch 2) runs as 3 chunked forwards + the one all-gather, at
+    world 2 -- the path the strong_1024 leg takes on 1 and 2 GPUs."""
+    p, lines = _run([sys.executable, BENCH, "--gpus", "2", "--batch", "2", "--strong-global", "10"] + SMALL)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads(lines[0])
+    (leg,) = out["strong_scaling"]
+    assert leg["global_batch"] == 10 and leg["per_rank_batch"] == [5, 5] and leg["value"] > 0
+
+
 def test_torchrun_launch():
     p, lines = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                      "--master-addr", "127.0.0.1", "--master-port", str(_port()), BENCH, "--gpus", "2",

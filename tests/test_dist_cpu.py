@@ -1,7 +1,9 @@
 """Multi-rank batch sharding + mask all-gather with the gloo backend on CPU,
 world_size 2 and 3.  The collective is the same call the bench's RCCL path makes
 (all_gather_into_tensor; gloo implements it on CPU), and the bench's N>1 step and timing loop
-(unet_mi355x.dist.sharded_mask_step / timed_steps, used verbatim by bench.py) run here with a
+(unet_mi355x.dist.sharded_mask_step / timed_steps: bench.py's step calls sharded_mask_step whenever a
+shard fits one forward, and runs the same forward per chunk + the same gather otherwise, which
+tests/test_bench_cpu.py::test_strong_legs_chunked_two_ranks covers) run here with a
 deterministic CPU stand-in for the per-rank forward (no GPU here)."""
 import os
 import socket

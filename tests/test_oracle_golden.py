@@ -116,3 +116,51 @@ def test_oracle_run_unet_matches_reference_golden():
             assert list(arr.shape) == list(z["crop_shape_" + k])
             if np.array_equal(masks[k], ref):
                 assert hashlib.sha256(arr.tobytes()).hexdigest() == str(z["crop_sha256_" + k])
+
+
+def _pretrained_sd(z):
+    sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
+    assert syn.state_dict_checksum(sd) == str(z["sd_sha256"]), "pretrained weight profile drifted"
+    return sd
+
+
+def test_pretrained_pages_are_the_bench_pages():
+    """The fixture pages are the bench's own pages (bench.gen_pages seed 1000, 64 unique pages),
+    quantised to uint8 as a photo delivers them (make_golden.quantised_pages)."""
+    import bench
+    z = np.load(os.path.join(GOLD, "pretrained_512_pages.npz"))
+    pages = bench.gen_pages(1000, 64, 512, 1, unique=64)[:, 0]
+    for j, i in enumerate(z["page_index"]):
+        q = (pages[i].astype(np.float64) * 255.0 + 0.5).astype(np.uint8)
+        assert np.array_equal(q, z["pages_u8"][j])
+
+
+def test_oracle_matches_reference_pretrained_512_pages():
+    """The oracle on the trained-like weight profile the bench's IoU claims use, against the
+    reference's own run_unet masks and logits for 4 of the bench's 512x512 pages."""
+    z = np.load(os.path.join(GOLD, "pretrained_512_pages.npz"))
+    sd = _pretrained_sd(z)
+    x = torch.from_numpy(np.repeat(z["pages_u8"][:, None].astype(np.float32) / 255.0, 3, axis=1))
+    lg = orc.unet_forward(sd, x).numpy()
+    for j in range(x.shape[0]):
+        assert hashlib.sha256(x[j:j + 1].numpy().tobytes()).hexdigest() == str(z[f"x_sha256_{j}"])
+        ref = z[f"logits_sub8_{j}"]
+        np.testing.assert_allclose(lg[j][:, ::8, ::8], ref, rtol=0, atol=2e-5 * max(1.0, float(np.abs(ref).max())))
+        masks = orc.masks_from_logits(lg[j])
+        for k in orc.FIELDS:
+            refm = np.unpackbits(z[f"maskbits_{k}_{j}"], axis=-1, bitorder="little").astype(bool)
+            assert orc.mask_iou(masks[k], refm) >= 0.9999, (j, k)
+
+
+def test_oracle_matches_reference_pretrained_1024_page():
+    """BASELINE config 5's resolution: one 1024x1024 page through the reference forward."""
+    z = np.load(os.path.join(GOLD, "pretrained_1024_page.npz"))
+    sd = _pretrained_sd(z)
+    x = torch.from_numpy(np.repeat(z["page_u8"][None, None].astype(np.float32) / 255.0, 3, axis=1))
+    lg = orc.unet_forward(sd, x).numpy()[0]
+    ref = z["logits_sub8"]
+    np.testing.assert_allclose(lg[:, ::8, ::8], ref, rtol=0, atol=2e-5 * max(1.0, float(np.abs(ref).max())))
+    masks = orc.masks_from_logits(lg)
+    for k in orc.FIELDS:
+        refm = np.unpackbits(z[f"maskbits_{k}"], axis=-1, bitorder="little").astype(bool)
+        assert orc.mask_iou(masks[k], refm) >= 0.9999, k

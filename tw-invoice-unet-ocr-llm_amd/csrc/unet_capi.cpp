@@ -808,7 +808,10 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
   const float* HW = sd.get("out_conv.weight", {ncls, 64, 1, 1}, err);
   const float* HB = HW ? sd.get("out_conv.bias", {ncls}, err) : nullptr;
   if (!HB) return fail(UNET_EKEY, err);
-  rc = upload(h, (void**)&h->head_w, HW, (size_t)ncls * 64 * 4);
+  // the 16-bit plans' 1x1 head runs on MFMA operands of conv1.3's type (weights rounded in the
+  // kernel; the bias stays fp32), so its weights must fit fp16 there too
+  rc = check_f16_range(h->L[C1B].dt, std::vector<double>(HW, HW + (size_t)ncls * 64), {}, "out_conv");
+  if (!rc) rc = upload(h, (void**)&h->head_w, HW, (size_t)ncls * 64 * 4);
   if (!rc) rc = upload(h, (void**)&h->head_b, HB, (size_t)ncls * 4);
   if (rc) return rc;
   h->loaded = true;
