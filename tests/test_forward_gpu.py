@@ -202,13 +202,15 @@ def test_masks_512_pretrained_weights():
         m.close()
 
 
-def test_batch256_bench_shape_invariance_and_iou():
+def test_batch256_bench_shape_invariance_and_iou(monkeypatch):
     """The batch the bench times (256 pages of 512x512, the bench's mixed plan, bit-packed
     masks): image i of the N=256 forward equals the same image run alone (N=1) and in the
     second half-batch (N=128, rank 1's shard of a 2-GPU run) bit for bit -- the persistent
     walkers wrap ~100x more often at N=256 than in the small tests --, and the masks of 4
-    sampled pages match the fp32 oracle at IoU >= 0.999."""
+    sampled pages match the fp32 oracle at IoU >= 0.999.  (N = 1 with the small-batch split-K
+    plan switched off: that plan accumulates in another order, test_small_batch_split_k_plan.)"""
     import bench
+    monkeypatch.setenv("UNET_MI355X_KSPLIT", "0")
     sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
     m = make_model(sd, 3, "mixed")
     x = torch.from_numpy(bench.gen_pages(1000, 256, 512, 3, unique=64)).to(DEV)
@@ -580,9 +582,13 @@ def _forced(cfg, up, sd, x, dtype, monkeypatch):
     monkeypatch.setenv("UNET_MI355X_CFG", ",".join(f"{i}:{cfg}" for i in range(17)) if cfg is not None else "")
     monkeypatch.setenv("UNET_MI355X_UPCFG", ",".join(f"{i}:{up}" for i in range(4)) if up is not None else "")
     monkeypatch.setenv("UNET_MI355X_FUSE_UP1", "0")
+    # families compared on the unsplit kernels: the small-batch split-K plan (N = 2 here) picks its
+    # slice count from each configuration's tile grid
+    monkeypatch.setenv("UNET_MI355X_KSPLIT", "0")
     m = make_model(sd, 3, dtype)
     st = _forward_state(m, x)
     m.close()
+    monkeypatch.delenv("UNET_MI355X_KSPLIT")
     return st
 
 
@@ -771,12 +777,14 @@ def test_reference_pages_in_bs256_mixed_batch():
     m.close()
 
 
-def test_reference_pages_in_bs32_fp32_batch_and_batch_invariance():
+def test_reference_pages_in_bs32_fp32_batch_and_batch_invariance(monkeypatch):
     """BASELINE config 2's shape at the drop-in's default precision (fp32, batch 32), pinned to the
     reference: the 4 reference pages at positions 0, 9, 20, 31 of the fp32 leg's batch meet IoU >=
     0.9999 and the fp32 logit tolerance; and every image of the N = 32 forward equals the same image
-    run alone (N = 1) bit for bit."""
+    run alone (N = 1) bit for bit (the small-batch split-K plan off: it is another accumulation order,
+    test_small_batch_split_k_plan)."""
     import bench
+    monkeypatch.setenv("UNET_MI355X_KSPLIT", "0")
     pos = (0, 9, 20, 31)
     x, z = _embed_reference_pages(bench.gen_pages(2000, 32, 512, 3), pos)
     sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
@@ -936,3 +944,42 @@ def test_run_unet_batch_equals_per_photo_calls():
             assert (c1[k] is None) == (c2[k] is None), k
             if c1[k] is not None:
                 assert np.array_equal(np.asarray(c1[k]), np.asarray(c2[k])), k
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "mixed", "bf16"])
+def test_small_batch_split_k_plan(dtype, monkeypatch):
+    """The small-batch plan (csrc/unet_capi.cpp layer_ksplit: the deep layers whose tile grid under-fills
+    the 256 CUs at N <= 4 run as K slices into fp32 partials + a slice-ordered reduction): engaged at
+    N = 1 (its partial buffer enlarges the workspace), bitwise repeatable, bitwise the same image at N =
+    1, 3 and 4 (the slice counts depend on the layer only), pinned to the reference masks and logits of
+    the trained-like pages (pretrained_512_pages.npz), and within TOL of the unsplit kernels
+    (UNET_MI355X_KSPLIT=0)."""
+    z = np.load(os.path.join(GOLD, "pretrained_512_pages.npz"))
+    x = torch.from_numpy(np.repeat(z["pages_u8"][:, None].astype(np.float32) / 255.0, 3, axis=1)).to(DEV)
+    sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
+    monkeypatch.setenv("UNET_MI355X_KSPLIT", "0")
+    m0 = make_model(sd, 3, dtype)
+    ws_unsplit = m0.native_handle(torch.device(DEV)).workspace_bytes(1, 512, 512)
+    with torch.no_grad():
+        lg_unsplit = m0(x[:1]).cpu().numpy()
+    m0.close()
+    monkeypatch.delenv("UNET_MI355X_KSPLIT")
+    m = make_model(sd, 3, dtype)
+    h = m.native_handle(torch.device(DEV))
+    assert h.workspace_bytes(1, 512, 512) > ws_unsplit, "no layer split at batch 1"
+    with torch.no_grad():
+        bits4, lg4 = m.forward_masks(x, packed=True, with_logits=True)
+        bits4, lg4 = bits4.clone(), lg4.clone()
+        b3, l3 = m.forward_masks(x[1:].contiguous(), packed=True, with_logits=True)
+        assert torch.equal(b3, bits4[1:]) and torch.equal(l3, lg4[1:]), "N=3 != N=4"
+        for i in range(4):
+            b1, l1 = m.forward_masks(x[i:i + 1].contiguous(), packed=True, with_logits=True)
+            assert torch.equal(b1, bits4[i:i + 1]) and torch.equal(l1, lg4[i:i + 1]), f"image {i}: N=1 != N=4"
+        b1b, l1b = m.forward_masks(x[:1], packed=True, with_logits=True)
+        assert torch.equal(l1b, lg4[:1]), "split-K forward not repeatable"
+    err = rel_err(lg4[:1].cpu().numpy(), lg_unsplit)
+    print(f"{dtype}: split vs unsplit logits rel err {err:.3e}")
+    assert err <= TOL[dtype]
+    _check_against_reference_pages(bits4.cpu().numpy(), lg4.cpu().numpy(), z, range(4), dtype,
+                                   {"fp32": 0.9999, "mixed": 0.999, "bf16": 0.995}[dtype])
+    m.close()

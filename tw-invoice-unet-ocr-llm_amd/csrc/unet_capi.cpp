@@ -89,7 +89,7 @@ struct ResampleStore {
 constexpr size_t kResampleCacheMax = 16;   // geometries kept (LRU)
 
 struct Buffers {
-  size_t tA, cat1, cat2, cat3, cat4, p1, p2, p3, p4, bnb, tB, mbits, xpx, total;  // byte offsets
+  size_t tA, cat1, cat2, cat3, cat4, p1, p2, p3, p4, bnb, tB, mbits, xpx, part, total;  // byte offsets
 };
 
 }  // namespace
@@ -130,6 +130,12 @@ struct unet_handle {
   bool capturing = false;        // inside unet_graph_create: no event record / wait in the stream
   void* comm = nullptr;          // RCCL communicator (unet_comm_init), ncclComm_t
   unsigned long long generation = 1;   // bumped whenever device pointers a graph captured change
+  // split-K of under-filled layers (small batches, layer_ksplit): the largest slice count
+  // (UNET_MI355X_KSPLIT; 0 or 1 = never split) and per-launch forced counts for A/B runs
+  // (UNET_MI355X_KSPLIT_FORCE="i:ks,...", i = 3x3 layer 0..16 or 17 + ConvTranspose 0..3; 0 = auto)
+  int ksplit_max = 32;
+  int ksplit_force[21] = {};
+  void* part = nullptr;   // the current forward's partial buffer (workspace region Buffers::part)
 };
 
 struct unet_graph {
@@ -198,7 +204,69 @@ DType level_dtype(int dtype, int level) {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-Buffers plan(DType dt, int N, int H, int W) {
+// Split-K over Cin for a layer whose grid of (pixel tile, row tile) blocks under-fills the chip --
+// the small-batch plan of the production call (inference.py: one photo per run_unet; at batch 1 the
+// 32^2 bottleneck has 16 ring blocks for 256 CUs).  KS slices run as independent blocks writing fp32
+// partials (EPI_PARTIAL) that launch_splitk_reduce adds to the bias in slice order (deterministic,
+// bitwise repeatable).  The plan applies to batches N <= kSmallBatch with KS chosen from the layer's
+// batch-1 geometry, so an image's outputs are bitwise the same for every N <= kSmallBatch (and, with
+// the unsplit kernels, for every N > kSmallBatch); the two regimes accumulate in different orders and
+// agree within the fp32-accumulation tolerance, not bit for bit.  KS is the power of two minimising a
+// two-term model: compute on min(blocks x KS, 256) CUs at the family's per-CU rate, plus the partials'
+// HBM round trip and one more launch.  Eligible: the 8-wave 128-row ring (16-bit plans) and the
+// LDS-halo family (fp32 plan, 3x3 and ConvTranspose) with a plain store, pool or scatter epilogue;
+// never the fused first conv, the head or the fused up1.
+constexpr int kSmallBatch = 4;
+int layer_ksplit(const unet_handle* h, int id, const Layer& L, int epi, int N, int Hl, int Wl) {
+  if (h->ksplit_max <= 1 || N <= 0 || N > kSmallBatch || Hl <= 0 || Wl <= 0) return 1;
+  const bool ring8 = L.cfg == CFG_RING8_R128 && L.dt != DType::F32 && L.taps == 9;
+  const bool halo = cfg_is_halo(L.cfg) && L.dt == DType::F32;
+  if (!(ring8 || halo)) return 1;
+  if (!(epi == EPI_STORE || epi == EPI_POOL || epi == EPI_UPSCATTER)) return 1;
+  const int chunk = 32;   // K slice granule: one 32-channel chunk (ring8 16-bit, halo fp32)
+  const int nch = L.cin / chunk;
+  if (L.cin % chunk) return 1;
+  const int tw = cfg_tile_w(L.cfg), th = cfg_tile_h(L.cfg);
+  // blocks of ONE image (the plan depends on the layer and resolution only, not on N)
+  const long long blocks = (long long)(L.ctot / cfg_rows(L.cfg)) * ((Hl + th - 1) / th) * ((Wl + tw - 1) / tw);
+  const int cap = ring8 ? 256 : 512;   // resident blocks: one 512-thread ring block / two halo blocks per CU
+  const double rate = ring8 ? 5.5e12 : 0.55e12, bw = 5e12, t_launch = 4e-6;   // per-CU FLOP/s, B/s
+  const double P = (double)Hl * Wl;
+  const double flops = 2.0 * L.ctot * L.cin * L.taps * P;
+  const int forced = h->ksplit_force[id];
+  if (forced > 0) return (forced <= nch && nch % forced == 0 && blocks * forced <= 8LL * cap) ? forced : 1;
+  int best = 1;
+  double tbest = flops / ((double)std::min<long long>(blocks, 256) * rate);
+  for (int ks = 2; ks <= h->ksplit_max && nch % ks == 0 && nch / ks >= (ring8 ? 2 : 1) && blocks * ks <= cap; ks *= 2) {
+    const double t = flops / ((double)std::min<long long>(blocks * ks, 256) * rate) + ks * P * L.ctot * 8.0 / bw + t_launch;
+    if (t < tbest) { tbest = t; best = ks; }
+  }
+  return best;
+}
+
+// Launch order of forward_impl with each launch's layer, epilogue and input level, for the split-K
+// plan's workspace bound (the largest partial buffer of one launch).
+size_t split_bytes(const unet_handle* h, int N, int H, int W) {
+  size_t m = 0;
+  auto one = [&](int id, const Layer& L, int epi, int lvl) {
+    const int Hl = H >> lvl, Wl = W >> lvl;
+    const int ks = layer_ksplit(h, id, L, epi, N, Hl, Wl);
+    if (ks > 1) m = std::max(m, (size_t)ks * N * Hl * Wl * L.ctot * 4);
+  };
+  for (int i = 0; i < 17; ++i) {
+    const bool pool = i == D1B || i == D2B || i == D3B || i == D4B;
+    int epi = pool ? EPI_POOL : i == C1B ? EPI_HEAD : EPI_STORE;
+    if (i == C2B && h->fuse_up1) epi = EPI_UPFUSE;
+    if (i == D1B && cfg_fused_in(h->L[D1B].cfg)) continue;
+    one(i, h->L[i], epi, kLayerLevel[i]);
+  }
+  for (int j = 0; j < 4; ++j)
+    if (!(j == 3 && h->fuse_up1)) one(17 + j, h->U[j], EPI_UPSCATTER, kUpLevel[j]);
+  return m;
+}
+
+Buffers plan(const unet_handle* h, int N, int H, int W) {
+  const DType dt = h->dt;
   const size_t e = dtype_size(dt);
   const size_t P = (size_t)N * H * W;  // full-resolution pixels
   Buffers b{};
@@ -223,6 +291,8 @@ Buffers plan(DType dt, int N, int H, int W) {
   // -- the latter also on a 16-bit plan whose down1.3 is overridden to a non-fused configuration)
   b.xpx = o;
   o = align256(o + P * 3 * 4);
+  b.part = o;   // split-K partials (small batches; 0 bytes when no launch splits)
+  o = align256(o + split_bytes(h, N, H, W));
   b.total = o;
   return b;
 }
@@ -703,6 +773,20 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     h->fuse_up1 = !(fz && fz[0] == '0') && !f32 && (c2b.cfg == CFG_RING_R128 || c2b.cfg == CFG_RING8_R128) &&
                   u1.dt == c2b.dt && u1.dto == c2b.dto;
   }
+  if (const char* ks = std::getenv("UNET_MI355X_KSPLIT")) h->ksplit_max = std::atoi(ks);
+  if (const char* kf = std::getenv("UNET_MI355X_KSPLIT_FORCE")) {   // "i:ks,..." (A/B runs)
+    std::string o(kf);
+    size_t pos = 0;
+    while (pos < o.size()) {
+      size_t end = o.find(',', pos);
+      if (end == std::string::npos) end = o.size();
+      const std::string item = o.substr(pos, end - pos);
+      const size_t colon = item.find(':');
+      const int li = colon == std::string::npos ? -1 : std::atoi(item.substr(0, colon).c_str());
+      if (li >= 0 && li < 21) h->ksplit_force[li] = std::atoi(item.substr(colon + 1).c_str());
+      pos = end + 1;
+    }
+  }
   build_labels(h);   // after every layer's configuration (3x3 and ConvTranspose) is final
   DeviceGuard g(cfg->device);
   hipError_t e = hipEventCreateWithFlags(&h->done, hipEventDisableTiming);
@@ -820,14 +904,14 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
 
 size_t unet_workspace_bytes(const unet_handle* h, int N, int H, int W) {
   if (!h || N <= 0 || H <= 0 || W <= 0) return 0;
-  return plan(h->dt, N, H, W).total;
+  return plan(h, N, H, W).total;
 }
 
 int unet_reserve(unet_handle* h, int N, int H, int W) {
   if (!h) return fail(UNET_EINVAL, "null handle");
   int rc = check_geometry(h, N, H, W);
   if (rc) return rc;
-  const size_t need = plan(h->dt, N, H, W).total;
+  const size_t need = plan(h, N, H, W).total;
   if (need <= h->ws_bytes) return UNET_OK;
   DeviceGuard g(h->cfg.device);
   ++h->generation;
@@ -883,6 +967,16 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.tiles_x = (W + cfg_tile_w(L.cfg) - 1) / cfg_tile_w(L.cfg);
   a.tiles_y = (H + cfg_tile_h(L.cfg) - 1) / cfg_tile_h(L.cfg);
   a.n_ct = L.ctot / cfg_rows(L.cfg);
+  const int id = (&L >= h->L && &L < h->L + 17) ? (int)(&L - h->L) : 17 + (int)(&L - h->U);
+  const int ks = layer_ksplit(h, id, L, epi, N, H, W);
+  if (ks > 1) {   // small-batch plan: K slices into fp32 partials, then the layer's epilogue over their sum
+    a.part = static_cast<float*>(h->part);
+    a.ksplit = ks;
+    hipError_t e = launch_igemm(L.dt, L.dt, L.dt, L.cfg, L.taps, EPI_PARTIAL, a, s);
+    if (e == hipSuccess) e = launch_splitk_reduce(L.dto, epi == EPI_POOL ? L.dtq : L.dto, epi, a, s);
+    if (e != hipSuccess) return fail(UNET_EHIP, std::string("split-K igemm launch: ") + hipGetErrorString(e));
+    return UNET_OK;
+  }
   hipError_t e = launch_igemm(L.dt, L.dto, epi == EPI_POOL ? L.dtq : L.dto, L.cfg, L.taps, epi, a, s);
   if (e != hipSuccess) return fail(UNET_EHIP, std::string("igemm launch: ") + hipGetErrorString(e));
   return UNET_OK;
@@ -901,12 +995,12 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   int rc = check_geometry(h, N, H, W);
   if (rc) return rc;
   // no allocation (and so no hidden device synchronisation) here: unet_reserve sizes the workspace
-  if (plan(h->dt, N, H, W).total > h->ws_bytes)
+  if (plan(h, N, H, W).total > h->ws_bytes)
     return fail(UNET_ESTATE, "workspace too small for this (N, H, W): call unet_reserve first");
   DeviceGuard g(h->cfg.device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   order_after_last(h, s);
-  const Buffers B = plan(h->dt, N, H, W);
+  const Buffers B = plan(h, N, H, W);
   char* ws = h->ws;
   auto buf = [&](size_t off) { return static_cast<void*>(ws + off); };
   if (boxes && (!masks || mask_kind == UNET_MASK_NONE)) {   // boxes only: bit masks into the workspace
@@ -918,6 +1012,7 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
 
   int li = 0;
   auto mark = [&]() { if (ev) (void)hipEventRecord(ev[li], s); ++li; };
+  h->part = buf(B.part);   // split-K partials of the small-batch plan (run_igemm, layer_ksplit)
   mark();
   // down1.net.0 (C -> 64): fused into down1.3 on the 16-bit ring path (fed by the pre-cast input),
   // a direct conv otherwise
@@ -1117,7 +1212,7 @@ int unet_debug_fetch(unet_handle* h, const char* name, float* dst, size_t* numel
   if (!h || !name) return fail(UNET_EINVAL, "null argument");
   if (!h->lastN) return fail(UNET_ESTATE, "no forward has run");
   const int N = h->lastN, H = h->lastH, W = h->lastW;
-  const Buffers B = plan(h->dt, N, H, W);
+  const Buffers B = plan(h, N, H, W);
   struct Src { size_t off; int level, C, ld, choff; };
   static const std::map<std::string, int> idx = {
       {"c1", 0}, {"p1", 1}, {"c2", 2}, {"p2", 3}, {"c3", 4}, {"p3", 5}, {"c4", 6}, {"p4", 7},

@@ -17,8 +17,10 @@ enum Epi : int {
   EPI_POOL = 1,     // EPI_STORE + fused 2x2/2 max-pool into a second NHWC tensor
   EPI_HEAD = 2,     // bias + ReLU kept in fp32 -> fused 1x1 out_conv -> logits / masks
   EPI_UPSCATTER = 3,// ConvTranspose2d(k2,s2): bias, no ReLU, pixel-shuffle store
-  EPI_UPFUSE = 4    // conv2.3 + up1 in one launch: bias + ReLU kept in registers as the B operand of
+  EPI_UPFUSE = 4,   // conv2.3 + up1 in one launch: bias + ReLU kept in registers as the B operand of
                     // the ConvTranspose2d GEMM (no store), whose output is scattered like EPI_UPSCATTER
+  EPI_PARTIAL = 5   // split-K (small batches): one K slice's fp32 accumulators, no bias, into
+                    // part[slice][pixel][Ctot]; launch_splitk_reduce applies the layer's own epilogue
 };
 
 // Mask output formats for EPI_HEAD.
@@ -57,6 +59,10 @@ struct IgemmArgs {
   // EPI_UPFUSE: the ConvTranspose2d's bias [4 * Cout / 2] in natural (a, b, o) row order; its
   // output goes to out2 (pixel stride ldo2, channels [0, Cout / 2)) at 2H x 2W
   const float* bias2;
+  // EPI_PARTIAL: K (= Cin chunks) split into ksplit equal slices; slice k of pixel p, row r at
+  // part[(k * N*H*W + p) * Ctot + r] (natural row order, fp32)
+  float* part;
+  int ksplit;
 };
 
 struct FirstConvArgs {
@@ -118,6 +124,10 @@ int cfg_limit();            // valid Cfg values of this build (ablation builds: 
 hipError_t launch_igemm(DType t, DType to, DType tq, int cfg, int taps, int epi, const IgemmArgs& a,
                         hipStream_t s);
 hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s);
+// Split-K reduction of an EPI_PARTIAL launch: out = epilogue(bias + part[0] + part[1] + ...) in
+// slice order, with the layer's epilogue epi (EPI_STORE / EPI_POOL / EPI_UPSCATTER) and its output
+// arguments (out, ldo, out_off, out2, ldo2, Cout) taken from `a`
+hipError_t launch_splitk_reduce(DType to, DType tq, int epi, const IgemmArgs& a, hipStream_t s);
 // Network input (fp32 or uint8 = value/255, NCHW or NHWC; include/unet_mi355x.h) -> element type
 // t, 4 channels per pixel [N][H][W][4] (input of the fused first conv of CFG_RING_FUSED_IN)
 hipError_t launch_x_to_px4(DType t, const void* x, int layout, int xdt, int N, int C, int H, int W, void* out,

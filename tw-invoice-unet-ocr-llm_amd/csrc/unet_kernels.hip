@@ -526,6 +526,28 @@ __device__ __forceinline__ void conv_epilogue(const IgemmArgs& a, const f32x4 (&
   }
 }
 
+// EPI_PARTIAL (split-K, small batches): the lane's 16 natural rows row0 + 16q .. + 15 of each of its
+// TP pixels (acc[t][p][e] = row 16q + 4t + e) as fp32 into slice `slice` of a.part: four 16-byte
+// stores per pixel, 256 contiguous bytes per pixel and 64-row group across the four lane rows.
+template <int TP, int TW>
+__device__ __forceinline__ void partial_store(const IgemmArgs& a, const f32x4 (&acc)[4][TP], int n, int oy0, int ox0,
+                                              int g0, int row0, int slice) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
+  const long long P = (long long)a.N * a.H * a.W;
+  float* base = a.part + (long long)slice * P * a.Ctot + row0 + 16 * q;
+#pragma unroll
+  for (int p = 0; p < TP; ++p) {
+    int py, px;
+    pix_of_w<TW>((g0 + p) * 16 + col, py, px);
+    const int oy = oy0 + py, ox = ox0 + px;
+    if (oy < a.H && ox < a.W) {
+      f32x4* d = reinterpret_cast<f32x4*>(base + ((long long)(n * a.H + oy) * a.W + ox) * a.Ctot);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) d[t] = acc[t][p];
+    }
+  }
+}
+
 
 // ---------------------------------------------------------------------------------
 // 3x3 conv with an LDS halo tile (the fp32 path; 128-byte K chunks)
@@ -685,8 +707,13 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
     const int b = blockIdx.x, x = b & 7, k = b >> 3;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
   }
+  // EPI_PARTIAL: block = (row tile, K slice, pixel tile); the slice covers Cin chunks c_lo .. c_lo + nch
+  constexpr bool PART = EPI == EPI_PARTIAL;
+  const int KS = PART ? a.ksplit : 1;
   const int ct = bid % a.n_ct;
   int mt = bid / a.n_ct;
+  const int kslice = PART ? mt % KS : 0;
+  if (PART) mt /= KS;
   const int tx = mt % a.tiles_x;
   mt /= a.tiles_x;
   const int ty = mt % a.tiles_y;
@@ -695,7 +722,8 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
 
   const int H = a.H, W = a.W;
   const int K = NTAP * a.Cin;
-  const int nch = a.Cin / BKE;
+  const int nch = a.Cin / BKE / KS;
+  const int c_lo = kslice * nch;
   const int S = NTAP * nch;
 
   const int w_chk = ((lane & 7) ^ ((lane >> 3) & 7)) * 16;
@@ -721,8 +749,8 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
       glds16(src, dst + j * 8 * 128);
     }
   };
-  auto issue_w = [&](int g) {   // K step g = (chunk, tap), weights [row][tap*Cin + c]
-    const int c = g / NTAP, tap = g - (g / NTAP) * NTAP;
+  auto issue_w = [&](int g) {   // K step g = (chunk, tap) of the slice, weights [row][tap*Cin + c]
+    const int c = c_lo + g / NTAP, tap = g - (g / NTAP) * NTAP;
     const size_t koff = ((size_t)tap * a.Cin + (size_t)c * BKE) * sizeof(T);
     char* dst = lds + WOFF + (g % NS) * WSLOT + wave * WI * 8 * 128;
 #pragma unroll
@@ -745,7 +773,7 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
   }
   const int px_lane = col & 7;
 
-  issue_halo(0);
+  issue_halo(c_lo);
   issue_w(0);
   if (NS == 3 && S > 1) issue_w(1);
   // epilogue parameters into LDS with plain loads, issued after the first DMAs so the two
@@ -796,15 +824,21 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
       if (wnext) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
     }
     if (tap == NTAP - 1 && c + 1 < nch) {   // every wave has finished reading the halo (barrier above)
-      issue_halo(c + 1);
+      issue_halo(c_lo + c + 1);
       wait_vm_barrier<0>();
     }
     if (++tap == NTAP) { tap = 0; ++c; }
   }
 #pragma unroll
-  for (int h = 0; h < TC / 4; ++h)
-    conv_epilogue<T, T, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16, wp * TP,
-                              ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h, headw_s, headb_s);
+  for (int h = 0; h < TC / 4; ++h) {
+    if constexpr (PART)
+      partial_store<TP, 16>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16, wp * TP,
+                            ct * BR + wr * 16 * TC + 64 * h, kslice);
+    else
+      conv_epilogue<T, T, TP, EPI>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * 16,
+                                   wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h, headw_s,
+                                   headb_s);
+  }
 }
 
 
@@ -1459,6 +1493,12 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   constexpr bool UPF = EPI == EPI_UPFUSE;
   static_assert(!UPF || (sizeof(T) == 2 && TC == 8 && TPS == 3 && WST == 0 && HS == 0), "fused ConvTranspose");
   constexpr int SU = UPF ? 4 : 0;
+  // EPI_PARTIAL (split-K, small batches): the walkers' items are (pixel tile, K slice) pairs, item
+  // m = tile m / KS, slice m % KS; the launcher makes n_slots a multiple of KS, so a walker keeps ONE
+  // slice (its weight ring cycles over that slice's steps) and its halo cursor starts at the slice's
+  // first chunk.  Accumulators start at zero (the reduction adds the bias).
+  constexpr bool PART = EPI == EPI_PARTIAL;
+  static_assert(!PART || (HS == 0 && WST == 0 && !UPF), "split-K: the streamed-weight ring");
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
   float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
   float* headw_s = bias_s + BR;
@@ -1479,12 +1519,15 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   const int ct = bid % a.n_ct;
   const int slot = bid / a.n_ct;
   const int n_slots = gridDim.x / a.n_ct;
-  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  const int KS = PART ? a.ksplit : 1;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x * KS;
   if (slot >= n_mt) return;
   const int items = (n_mt - slot + n_slots - 1) / n_slots;
+  const int kslice = PART ? slot % KS : 0;
 
   const int H = a.H, W = a.W;
-  const int nch = a.Cin / BKE;
+  const int nch = a.Cin / BKE / KS;   // 32-channel chunks per tile (of this walker's K slice)
+  const int c_lo = kslice * nch;
   const int S = SPC * nch;       // conv steps per tile
   const int ST = S + SU;         // ring steps per tile
   const int total = items * ST;
@@ -1511,13 +1554,14 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 
   // weights of row tile ct in step order (the 4-wave ring's packing): piece j of a step = rows
   // 16j .. 16j+15; per lane one 16-byte chunk of row 16j + lane/4 at position chunk ^ ((row>>1)&3)
-  const char* wblk = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * ST * SLOT + (lane >> 2) * 64 +
-                     (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
+  const char* wblk = reinterpret_cast<const char*>(a.wgt) + ((size_t)ct * ST * KS + (size_t)kslice * S) * SLOT +
+                     (lane >> 2) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
   const char* in = reinterpret_cast<const char*>(a.in);
   const char* zero = reinterpret_cast<const char*>(a.zero);
 
   auto tile_of = [&](int i, int& n, int& ty, int& tx) {
     int mt = slot + i * n_slots;
+    if (PART) mt /= KS;
     tx = mt % a.tiles_x;
     mt /= a.tiles_x;
     ty = mt % a.tiles_y;
@@ -1539,7 +1583,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         const bool ok = row < HP && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
         const int chk = ((lane & 3) ^ (hx & 3)) << 4;
         const long long pix = pix0 + (long long)(hy - 1) * W + (hx - 1);
-        hsrc[j] = ok ? in + pix * a.ldi * (long long)sizeof(T) + chk : zero + chk;
+        // (+ the K slice's first chunk; the zero page covers all 32 chunks of a 1024-channel input)
+        hsrc[j] = (ok ? in + pix * a.ldi * (long long)sizeof(T) + chk : zero + chk) + c_lo * 64;
       }
     }
     const uint32_t dst = lds0 + (hq_seq & 1) * HALO_BYTES + wave * HI * 1024;
@@ -1577,7 +1622,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 #pragma unroll
     for (int t = 0; t < TC; ++t) {
       if (t < t0 || t >= t1) continue;
-      const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias_s + 64 * (t / 4) + 16 * q + 4 * (t % 4));
+      const f32x4 b4 = PART ? f32x4{0.f, 0.f, 0.f, 0.f}
+                            : *reinterpret_cast<const f32x4*>(bias_s + 64 * (t / 4) + 16 * q + 4 * (t % 4));
 #pragma unroll
       for (int p = 0; p < TP; ++p) acc[t][p] = b4;
     }
@@ -1988,7 +2034,10 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       // issued after them) retires them under that step's MFMAs.
 #pragma unroll
       for (int h = 0; h < TC / 4; ++h) {
-        if constexpr (ABL == 5) {
+        if constexpr (PART) {
+          partial_store<TP, TW>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16, tx * TW, wp * TP,
+                                ct * BR + 64 * h, kslice);
+        } else if constexpr (ABL == 5) {
 #pragma unroll
           for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -2023,9 +2072,12 @@ static hipError_t launch_ring8(const IgemmArgs& a, hipStream_t s) {
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + G::TW - 1) / G::TW) return hipErrorInvalidValue;
   if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
   if (WST && (9 / TPS) * (a.Cin / G::BKE) > G::WST_STEPS) return hipErrorInvalidValue;
-  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  const int KS = EPI == EPI_PARTIAL ? a.ksplit : 1;
+  if (KS < 1 || a.Cin % (G::BKE * KS) || (EPI == EPI_PARTIAL && !a.part)) return hipErrorInvalidValue;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x * KS;   // items: (pixel tile, K slice)
   int n_slots = kNumCUs / a.n_ct;   // one 512-thread block per CU
-  if (n_slots < 1) n_slots = 1;
+  n_slots -= n_slots % KS;          // every walker keeps one K slice (n_mt is a multiple of KS)
+  if (n_slots < KS) n_slots = KS;
   if (n_slots > n_mt) n_slots = n_mt;
   hipLaunchKernelGGL((conv3x3_ring8_kernel<T, TCW, NS, EPI, TPS, WST, TO, TQ, HS, ABL>), dim3(a.n_ct * n_slots), dim3(512),
                      0, s, a);
@@ -2325,7 +2377,10 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   using G = HaloGeom<T, WR, WPX, TCW, NS, KT>;
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
   if (a.Cin % G::BKE || a.Ctot % G::BR || a.n_ct != a.Ctot / G::BR) return hipErrorInvalidValue;
-  const long long nb = (long long)a.n_ct * a.N * a.tiles_y * a.tiles_x;   // one block per (row tile, pixel tile)
+  const int KS = EPI == EPI_PARTIAL ? a.ksplit : 1;
+  if (KS < 1 || a.Cin % (G::BKE * KS) || (EPI == EPI_PARTIAL && !a.part)) return hipErrorInvalidValue;
+  // one block per (row tile, K slice, pixel tile)
+  const long long nb = (long long)a.n_ct * KS * a.N * a.tiles_y * a.tiles_x;
   if (nb <= 0 || nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, NS, KT, EPI>), dim3((unsigned)nb), dim3(64 * WR * WPX), 0,
                      s, a);
@@ -2386,6 +2441,17 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
         return launch_ring8<T, 8, 3, EPI_UPFUSE, 3, 0, TO, TQ>(a, s);
     }
     return hipErrorInvalidValue;
+  } else if constexpr (EPI == EPI_PARTIAL) {   // split-K slices: the LDS-halo family and the 8-wave 128-row ring
+    if constexpr (ABL == 0) {
+      switch (cfg) {
+        case CFG_HALO_R64_W4: if constexpr (sizeof(T) == 4) return launch_halo<T, 1, 4, 4, 3, EPI, 3>(a, s); break;
+        case CFG_HALO_R64_W8: if constexpr (sizeof(T) == 4) return launch_halo<T, 1, 8, 4, 3, EPI, 3>(a, s); break;
+        case CFG_HALO_R128: if constexpr (sizeof(T) == 4) return launch_halo<T, 1, 4, 8, 2, EPI, 3>(a, s); break;
+        case CFG_RING8_R128: if constexpr (sizeof(T) == 2) return launch_ring8<T, 8, 3, EPI, 3, 0, T, T>(a, s); break;
+        default: break;
+      }
+    }
+    return hipErrorInvalidValue;
   } else {
   if (EPI == EPI_HEAD && cfg_rows(cfg) != 64) return hipErrorInvalidValue;   // the head needs all 64 channels
   if constexpr (ABL != 0) {   // ablation builds: the ring configurations only
@@ -2426,7 +2492,7 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
       if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
       break;
     case CFG_RING8_R128: if constexpr (EPI != EPI_HEAD) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ>(a, s); break;
-    case CFG_RING8_R64_T9: return launch_ring8<T, 4, 2, EPI, 9, 0, TO, TQ>(a, s);
+    case CFG_RING8_R64_T9: if constexpr (EPI != EPI_PARTIAL) return launch_ring8<T, 4, 2, EPI, 9, 0, TO, TQ>(a, s); break;
     case CFG_RING8_R64_WS: return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
     case CFG_RING8_FUSED_IN:
       if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ, 1>(a, s);
@@ -2438,8 +2504,12 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
 }
 
 // ConvTranspose2d(k2, s2) layers (1-tap GEMM + pixel-shuffle scatter).  TO = output type.
-template <typename T, typename TO>
+template <typename T, typename TO, int EPI = EPI_UPSCATTER>
 static hipError_t launch_up(int cfg, const IgemmArgs& a, hipStream_t s) {
+  if constexpr (EPI == EPI_PARTIAL) {   // split-K slices of the LDS-halo ConvTranspose (the fp32 path)
+    if (cfg == CFG_HALO_R128) return launch_halo<T, 1, 4, 8, 2, EPI_PARTIAL, 1>(a, s);
+    return hipErrorInvalidValue;
+  }
   switch (cfg) {
     case CFG_HALO_R128:
       if constexpr (std::is_same<T, TO>::value) return launch_halo<T, 1, 4, 8, 2, EPI_UPSCATTER, 1>(a, s);
@@ -2478,10 +2548,17 @@ static hipError_t launch_typed(int cfg, int taps, int epi, const IgemmArgs& a, h
       case EPI_POOL: return launch_3x3<T, TO, TQ, EPI_POOL>(cfg, a, s);
       case EPI_HEAD: return launch_3x3<T, TO, TQ, EPI_HEAD>(cfg, a, s);
       case EPI_UPFUSE: return launch_3x3<T, TO, TQ, EPI_UPFUSE>(cfg, a, s);
+      case EPI_PARTIAL:
+        if constexpr (std::is_same<T, TO>::value && std::is_same<T, TQ>::value) return launch_3x3<T, T, T, EPI_PARTIAL>(cfg, a, s);
+        return hipErrorInvalidValue;
       default: return hipErrorInvalidValue;
     }
   }
   if (taps == 1 && epi == EPI_UPSCATTER) return launch_up<T, TO>(cfg, a, s);
+  if (taps == 1 && epi == EPI_PARTIAL) {
+    if constexpr (std::is_same<T, float>::value && std::is_same<T, TO>::value) return launch_up<T, T, EPI_PARTIAL>(cfg, a, s);
+    return hipErrorInvalidValue;
+  }
   return hipErrorInvalidValue;
 }
 
@@ -2533,6 +2610,116 @@ hipError_t launch_first_conv(DType t, const FirstConvArgs& a, hipStream_t s) {
     case DType::F32: return first_t<float>(a, s);
     case DType::BF16: return first_t<__bf16>(a, s);
     case DType::F16: return first_t<_Float16>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------------
+// split-K reduction (small batches: layers whose tile grid under-fills the 256 CUs run as KS
+// independent K slices writing fp32 partials, EPI_PARTIAL)
+// ---------------------------------------------------------------------------------
+// One thread = 8 rows of one output pixel (EPI_STORE, EPI_UPSCATTER: input pixel) or of one 2x2
+// pooling window (EPI_POOL).  The slices are added to the bias in slice order (deterministic), then
+// the epilogue the layer's own kernel applies (conv_epilogue): NaN-propagating ReLU and TO stores;
+// for EPI_POOL also the window max of the ReLU outputs as TQ; for EPI_UPSCATTER the pixel-shuffle
+// store without ReLU.  Reads 32 contiguous bytes per thread and slice (coalesced across threads).
+template <typename T>
+__device__ __forceinline__ void store8(T* dst, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    f32x4* d = reinterpret_cast<f32x4*>(dst);
+    d[0] = f32x4{v[0], v[1], v[2], v[3]};
+    d[1] = f32x4{v[4], v[5], v[6], v[7]};
+  } else {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    t8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (T)v[i];
+    *reinterpret_cast<uint4*>(dst) = __builtin_bit_cast(uint4, o);
+  }
+}
+
+template <typename TO, typename TQ, int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const IgemmArgs a) {
+  const int R8 = a.Ctot / 8;
+  const int H = a.H, W = a.W;
+  const int Hs = EPI == EPI_POOL ? H / 2 : H, Ws = EPI == EPI_POOL ? W / 2 : W;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)a.N * Hs * Ws * R8) return;
+  const int r0 = 8 * (int)(idx % R8);
+  long long pix = idx / R8;
+  const int x = (int)(pix % Ws);
+  pix /= Ws;
+  const int y = (int)(pix % Hs);
+  const int n = (int)(pix / Hs);
+  const long long slice = (long long)a.N * H * W * a.Ctot;
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + r0), b1 = *reinterpret_cast<const f32x4*>(a.bias + r0 + 4);
+  auto reduce = [&](int yy, int xx, float (&v)[8]) {
+    const float* src = a.part + ((long long)(n * H + yy) * W + xx) * a.Ctot + r0;
+    f32x4 s0 = b0, s1 = b1;
+    for (int k = 0; k < a.ksplit; ++k) {
+      s0 += *reinterpret_cast<const f32x4*>(src + k * slice);
+      s1 += *reinterpret_cast<const f32x4*>(src + k * slice + 4);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = s0[e]; v[4 + e] = s1[e]; }
+  };
+  if constexpr (EPI == EPI_UPSCATTER) {
+    const int ab = r0 / a.Cout, o0 = r0 - ab * a.Cout;   // 8 rows of one (a, b) quadrant (Cout % 8 == 0)
+    const int Y = 2 * y + (ab >> 1), X = 2 * x + (ab & 1);
+    float v[8];
+    reduce(y, x, v);
+    store8<TO>(reinterpret_cast<TO*>(a.out) + ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0, v);
+  } else if constexpr (EPI == EPI_POOL) {
+    float m[8];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int yy = 2 * y + (d >> 1), xx = 2 * x + (d & 1);
+      float v[8];
+      reduce(yy, xx, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = relu_nan(v[e]);
+        m[e] = d == 0 ? v[e] : max_nan(m[e], v[e]);
+      }
+      store8<TO>(reinterpret_cast<TO*>(a.out) + ((long long)(n * H + yy) * W + xx) * a.ldo + a.out_off + r0, v);
+    }
+    store8<TQ>(reinterpret_cast<TQ*>(a.out2) + ((long long)(n * Hs + y) * Ws + x) * a.ldo2 + r0, m);
+  } else {
+    float v[8];
+    reduce(y, x, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = relu_nan(v[e]);
+    store8<TO>(reinterpret_cast<TO*>(a.out) + ((long long)(n * H + y) * W + x) * a.ldo + a.out_off + r0, v);
+  }
+}
+
+template <typename TO, typename TQ, int EPI>
+static hipError_t splitk_reduce_t(const IgemmArgs& a, hipStream_t s) {
+  if (a.Ctot % 8 || (EPI == EPI_UPSCATTER && a.Cout % 8) || a.ksplit < 1 || !a.part) return hipErrorInvalidValue;
+  const long long threads = (long long)a.N * (EPI == EPI_POOL ? (a.H / 2) * (a.W / 2) : a.H * a.W) * (a.Ctot / 8);
+  if (threads <= 0 || (threads + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((splitk_reduce_kernel<TO, TQ, EPI>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_splitk_reduce(DType to, DType tq, int epi, const IgemmArgs& a, hipStream_t s) {
+  if (epi == EPI_POOL) {
+    if (to == DType::F32 && tq == DType::F32) return splitk_reduce_t<float, float, EPI_POOL>(a, s);
+    if (to == DType::BF16 && tq == DType::BF16) return splitk_reduce_t<__bf16, __bf16, EPI_POOL>(a, s);
+    if (to == DType::F16 && tq == DType::F16) return splitk_reduce_t<_Float16, _Float16, EPI_POOL>(a, s);
+    if (to == DType::F16 && tq == DType::BF16) return splitk_reduce_t<_Float16, __bf16, EPI_POOL>(a, s);
+    return hipErrorInvalidValue;
+  }
+  if (epi != EPI_STORE && epi != EPI_UPSCATTER) return hipErrorInvalidValue;
+  switch (to) {
+    case DType::F32:
+      return epi == EPI_STORE ? splitk_reduce_t<float, float, EPI_STORE>(a, s) : splitk_reduce_t<float, float, EPI_UPSCATTER>(a, s);
+    case DType::BF16:
+      return epi == EPI_STORE ? splitk_reduce_t<__bf16, __bf16, EPI_STORE>(a, s)
+                              : splitk_reduce_t<__bf16, __bf16, EPI_UPSCATTER>(a, s);
+    case DType::F16:
+      return epi == EPI_STORE ? splitk_reduce_t<_Float16, _Float16, EPI_STORE>(a, s)
+                              : splitk_reduce_t<_Float16, _Float16, EPI_UPSCATTER>(a, s);
   }
   return hipErrorInvalidValue;
 }
