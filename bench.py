@@ -22,8 +22,9 @@ per rank) -- as `strong_scaling`.
 Rank 0 prints ONE JSON line.  Extra fields: roofline (dominant kernel, HIP-event timed inside
 this run), cpu_baseline (the oracle on this host's cores, bounded sample), fp32 (BASELINE
 config 2: batch 32, 512^2, the drop-in's default precision, against the 157.3 TF fp32 MFMA
-peak), latency_bs1 (the drop-in run_unet and the batch-1 forward at the drop-in default fp32
-and at the bench plan), kernels (per-instantiation time breakdown).
+peak), cfg5 (BASELINE config 5 per GPU: 1024^2, fp16, batch 64), latency_bs1 (the drop-in run_unet
+and the batch-1 forward at the drop-in default fp32 and at the bench plan, with a per-layer
+breakdown), kernels (per-instantiation time breakdown).
 """
 from __future__ import annotations
 
@@ -419,8 +420,12 @@ def kernel_table(runner, model, x, masks, B, S, C, dtype, traffic_json):
         tj = json.load(open(traffic_json))
         traffic = tj.get(dom_name, {}).get("hbm_bytes_per_launch")
         meta = tj.get("_meta", {})
+        from unet_mi355x.native import kernel_sources_sha256
+        stamped = meta.get("kernel_sources_sha256")
         source = {"file": os.path.relpath(traffic_json, REPO), "commit": meta.get("source_commit"),
-                  "collected": meta.get("collected")}
+                  "collected": meta.get("collected"), "kernel_sources_sha256": stamped,
+                  # do the PMC counters describe the kernels timed here? (None: not stamped, older summary)
+                  "kernel_sources_match": None if stamped is None else stamped == kernel_sources_sha256()}
     roofline = {"bound": "mfma", "kernel": dom_name, "symbol": mangled(dom_name),
                 "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": source,
@@ -431,10 +436,12 @@ def kernel_table(runner, model, x, masks, B, S, C, dtype, traffic_json):
     return kernels, layer_ms, roofline, total_gflop, sum(ms)
 
 
-def cpu_baseline(args, sd, x, masks, C, S):
+def cpu_baseline(args, sd, x, masks, C, S, extra=()):
     """The oracle (fp32 eager torch restating unet_model.py / inference.py) on this host's
     cores: batch-1 forward (images/s + the mask IoU of the GPU masks), batch-8 forward, and
-    run_unet end to end (model load + resize + forward + masks + crops, inference.py:50-129)."""
+    run_unet end to end (model load + resize + forward + masks + crops, inference.py:50-129).
+    extra: (name, x [1, C, h, w] CPU, bit-packed GPU masks [1, 3, h, w/8] CPU, GPU dtype) of other
+    legs, whose masks are compared with the oracle's as `<name>_iou_vs_cpu`."""
     from PIL import Image
     from oracle import unet_oracle as orc
     threads, info = host_cores()
@@ -467,7 +474,14 @@ def cpu_baseline(args, sd, x, masks, C, S):
         t0 = time.perf_counter()
         orc.load_model_state(ck)
         t_load = time.perf_counter() - t0
-    return {"value": round(done / t_bs1, 4), "unit": "images/s", "cores": threads, "kind": "port",
+    more = {}
+    for name, xe, me, dte in extra:
+        ref = orc.masks_from_logits(orc.unet_forward(sd_cpu, xe).numpy()[0])
+        got = np.unpackbits(me.numpy()[0], axis=-1, bitorder="little").astype(bool)
+        ie = [orc.mask_iou(got[i], ref[f]) for i, f in enumerate(orc.FIELDS)]
+        more[f"{name}_iou_vs_cpu"] = {"min": round(min(ie), 5), "mean": round(float(np.mean(ie)), 5), "images": 1,
+                                      "size": int(xe.shape[-1]), "gpu_dtype": dte}
+    return {**more, "value": round(done / t_bs1, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{done} of the bench images, batch 1, {S}x{S}, fp32 eager torch (oracle/unet_oracle.py), "
                       f"{threads} threads",
             "host": info,
@@ -499,6 +513,31 @@ def fp32_leg(args, runner, dev):
     model.close()
     del x, masks
     return out
+
+
+def cfg5_leg(args, runner, dev):
+    """BASELINE config 5 on one GPU: the reference's 5-level UNet(3,3) at 1024x1024, fp16 storage with
+    fp32 accumulation, 64 images per GPU (config 5's per-rank share of batch 512 over 8 GPUs), fused
+    bit-packed masks, timed like the headline (HIP events per launch for the roofline; traffic from
+    profiles/pmc_fp16_bs64_1024.json).  Returns (summary, first page, its masks) for the CPU check."""
+    B, S, C = args.cfg5_batch, 1024, args.channels
+    model = runner.make_model("fp16")
+    runner.reserve(B, S, model)
+    x = torch.from_numpy(gen_pages(4000, B, S, C, unique=16)).to(dev)
+    masks = torch.empty((B, 3, S, S // 8), dtype=torch.uint8, device=dev)
+    seg = runner.segment_fn(model)
+    leg = {"step": lambda: seg(x, masks), "n_total": B}
+    t = time_leg(leg, args.cfg5_steps, 2, torch.cuda.synchronize, dev)
+    kernels, layer_ms, roof, gflop, _ = kernel_table(runner, model, x, masks, B, S, C, "fp16", "auto")
+    out = {"config": f"BASELINE config 5 shape per GPU: batch {B}, {S}x{S}, UNet({C},3) (5 resolution levels), "
+                     "fp16 storage + fp32 accumulation, fused bit-packed masks",
+           "value": round(t["value"], 2), "unit": "images/s", "ms_per_step": round(t["ms_per_step"], 3),
+           "steps": args.cfg5_steps, "whole_step_tflops": round(gflop / t["ms_per_step"], 1),
+           "roofline": roof, "kernels": kernels, "layer_ms": layer_ms}
+    page, mk = x[:1].cpu(), masks[:1].cpu()
+    model.close()
+    del x, masks
+    return out, page, mk
 
 
 def gpu_latency(args, runner, dev):
@@ -543,6 +582,11 @@ def gpu_latency(args, runner, dev):
             e1.record()
             torch.cuda.synchronize()
             out["forward_bs1_eager_ms"] = round(e0.elapsed_time(e1) / reps, 4)
+            # per-layer breakdown of the batch-1 forward (HIP events around every launch slot; a split-K
+            # layer's slot holds its partial launch + reduction; up1's slot is empty when fused)
+            for _ in range(3):
+                lms = h.forward_timed(x1, None, m1, native.MASK_BITS, runner.stream)
+            out["forward_bs1_layer_ms"] = {e[0]: round(t, 4) for e, t in zip(LAUNCHES, lms)}
             g = h.graph(x1, None, m1, native.MASK_BITS)
             m1.zero_()
             g.launch(runner.stream)
@@ -582,6 +626,9 @@ def main():
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 config-2 leg")
     ap.add_argument("--fp32-batch", type=int, default=32)
     ap.add_argument("--fp32-steps", type=int, default=5)
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the BASELINE config 5 leg (1024^2 fp16 bs64)")
+    ap.add_argument("--cfg5-batch", type=int, default=64)
+    ap.add_argument("--cfg5-steps", type=int, default=5)
     ap.add_argument("--standin", action="store_true",
                     help="CPU stand-in forward over gloo (tests: the launcher, sharding and timing without a GPU)")
     ap.add_argument("--traffic-json", default="auto",
@@ -656,12 +703,16 @@ def main():
         roofline["whole_step_tflops"] = whole
 
     # ---- rank 0 at N=1: fp32 config-2 leg, CPU baseline, batch-1 latency
-    fp32 = cpu = lat = None
+    fp32 = cfg5 = cpu = lat = None
+    extra = []
     solo = rank == 0 and world == 1 and not args.standin
     if solo and not args.no_fp32 and S == 512 and args.dtype != "fp32":
         fp32 = fp32_leg(args, runner, dev)
+    if solo and not args.no_cfg5 and S == 512:
+        cfg5, page5, masks5 = cfg5_leg(args, runner, dev)
+        extra.append(("cfg5", page5, masks5, "fp16"))
     if solo and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, runner.sd, main_leg["x"], main_leg["gather"].local, C, S)
+        cpu = cpu_baseline(args, runner.sd, main_leg["x"], main_leg["gather"].local, C, S, extra)
     if solo and not args.no_latency and S == 512 and C == 3:
         lat = gpu_latency(args, runner, dev)
 
@@ -677,7 +728,7 @@ def main():
                                    f"threshold bit-packed masks" + (" + RCCL all-gather" if world > 1 else ""),
                        "global_batch": main_leg["n_total"], "per_gpu_batch": B, "image": S,
                        "parallelism": f"dp{world}", "precision_plan": PLAN[args.dtype]},
-            "roofline": roofline, "cpu_baseline": cpu, "strong_scaling": strong_out, "fp32": fp32,
+            "roofline": roofline, "cpu_baseline": cpu, "strong_scaling": strong_out, "fp32": fp32, "cfg5": cfg5,
             "latency_bs1": lat, "step_ms": res.get("step_ms"), "host_step_ms": res["host_step_ms"],
             "kernels": kernels, "layer_ms": layer_ms,
         }

@@ -106,8 +106,9 @@ def main():
         k["gflop"] += flops / 1e9
         k["algo_bytes"] += algo
     import time
+    from unet_mi355x.native import kernel_sources_sha256
     out = {"_meta": {"source_commit": a.commit, "collected": time.strftime("%Y-%m-%d"), "dir": a.dir,
-                     "batch": a.batch, "size": a.size}}
+                     "batch": a.batch, "size": a.size, "kernel_sources_sha256": kernel_sources_sha256()}}
     for name, k in agg.items():
         n = k["launches"]
         out[name] = {"launches": int(n), "hbm_bytes_per_launch": (k["hbm_read_bytes"] + k["hbm_write_bytes"]) / n,

@@ -69,6 +69,21 @@ SIGNATURES = {
 
 _lib = None
 _lib_lock = threading.Lock()
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+
+
+def kernel_sources_sha256() -> str:
+    """sha256 over the library's sources (csrc/*.hip, *.cpp, *.h, in name order): stamped into
+    the PMC summaries (tools/pmc_summary.py) so bench.py can tell whether a traffic figure was
+    collected on the kernels it is timing."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in sorted(os.listdir(CSRC)):
+        if name.endswith((".hip", ".cpp", ".h")):
+            h.update(name.encode())
+            with open(os.path.join(CSRC, name), "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()
 
 
 def load_library(path: str = LIB_PATH):
