@@ -135,6 +135,7 @@ struct unet_handle {
   // (UNET_MI355X_KSPLIT_FORCE="i:ks,...", i = 3x3 layer 0..16 or 17 + ConvTranspose 0..3; 0 = auto)
   int ksplit_max = 32;
   int ksplit_force[21] = {};
+  unsigned xcd_rows = 0;   // bit i: 3x3 layer i walks with XCD-owned row tiles (UNET_MI355X_XCDROWS="i,...")
   void* part = nullptr;   // the current forward's partial buffer (workspace region Buffers::part)
 };
 
@@ -774,6 +775,14 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
                   u1.dt == c2b.dt && u1.dto == c2b.dto;
   }
   if (const char* ks = std::getenv("UNET_MI355X_KSPLIT")) h->ksplit_max = std::atoi(ks);
+  if (const char* xr = std::getenv("UNET_MI355X_XCDROWS")) {   // "i,j,..." 3x3 layer indices (A/B runs)
+    for (const char* p = xr; *p;) {
+      const int li = std::atoi(p);
+      if (li >= 0 && li < 17) h->xcd_rows |= 1u << li;
+      while (*p && *p != ',') ++p;
+      if (*p == ',') ++p;
+    }
+  }
   if (const char* kf = std::getenv("UNET_MI355X_KSPLIT_FORCE")) {   // "i:ks,..." (A/B runs)
     std::string o(kf);
     size_t pos = 0;
@@ -968,6 +977,7 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.tiles_y = (H + cfg_tile_h(L.cfg) - 1) / cfg_tile_h(L.cfg);
   a.n_ct = L.ctot / cfg_rows(L.cfg);
   const int id = (&L >= h->L && &L < h->L + 17) ? (int)(&L - h->L) : 17 + (int)(&L - h->U);
+  a.xcd_rows = id < 17 ? (int)((h->xcd_rows >> id) & 1u) : 0;
   const int ks = layer_ksplit(h, id, L, epi, N, H, W);
   if (ks > 1) {   // small-batch plan: K slices into fp32 partials, then the layer's epilogue over their sum
     a.part = static_cast<float*>(h->part);

@@ -1510,14 +1510,21 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   const int lane = tid & 63;
   const int wp = wave;   // all 8 waves split the pixels; each covers all BR rows
 
-  int bid;
-  {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one pixel-tile walker
+  int ct, slot;
+  if (a.xcd_rows && (gridDim.x & 7) == 0 && 8 % a.n_ct == 0) {
+    // XCD-owned row tiles (blocks b and b + 8 share an XCD): XCD label x runs row tile x mod n_ct for
+    // a contiguous range of walkers, so its L2 streams n_ct / 8 of the weights -- and re-reads every
+    // pixel tile's halo once per row tile instead of once (bijective: gridDim.x = 8 q = n_ct n_slots)
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    ct = x % a.n_ct;
+    slot = (x / a.n_ct) * (int)(gridDim.x >> 3) + k;
+  } else {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one pixel-tile walker
     const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
     const int b = blockIdx.x, x = b & 7, k = b >> 3;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+    const int bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+    ct = bid % a.n_ct;
+    slot = bid / a.n_ct;
   }
-  const int ct = bid % a.n_ct;
-  const int slot = bid / a.n_ct;
   const int n_slots = gridDim.x / a.n_ct;
   const int KS = PART ? a.ksplit : 1;
   const int n_mt = a.N * a.tiles_y * a.tiles_x * KS;
