@@ -136,6 +136,7 @@ struct unet_handle {
   int ksplit_max = 32;
   int ksplit_force[21] = {};
   unsigned xcd_rows = 0;   // bit i: 3x3 layer i walks with XCD-owned row tiles (UNET_MI355X_XCDROWS="i,...")
+  int prio_hi = 0;         // UNET_MI355X_PRIO=1: waves 4-7 of the 8-wave kernels at s_setprio 1 (A/B option)
   void* part = nullptr;   // the current forward's partial buffer (workspace region Buffers::part)
 };
 
@@ -775,6 +776,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
                   u1.dt == c2b.dt && u1.dto == c2b.dto;
   }
   if (const char* ks = std::getenv("UNET_MI355X_KSPLIT")) h->ksplit_max = std::atoi(ks);
+  if (const char* pr = std::getenv("UNET_MI355X_PRIO")) h->prio_hi = std::atoi(pr) != 0;
   if (const char* xr = std::getenv("UNET_MI355X_XCDROWS")) {   // "i,j,..." 3x3 layer indices (A/B runs)
     for (const char* p = xr; *p;) {
       const int li = std::atoi(p);
@@ -978,6 +980,7 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.n_ct = L.ctot / cfg_rows(L.cfg);
   const int id = (&L >= h->L && &L < h->L + 17) ? (int)(&L - h->L) : 17 + (int)(&L - h->U);
   a.xcd_rows = id < 17 ? (int)((h->xcd_rows >> id) & 1u) : 0;
+  a.prio_hi = h->prio_hi;
   const int ks = layer_ksplit(h, id, L, epi, N, H, W);
   if (ks > 1) {   // small-batch plan: K slices into fp32 partials, then the layer's epilogue over their sum
     a.part = static_cast<float*>(h->part);

@@ -1506,6 +1506,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar: the DMA addresses stay in SGPRs
+  if (a.prio_hi && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const uint32_t lds0 = lds_addr_of(lds);
   const int lane = tid & 63;
   const int wp = wave;   // all 8 waves split the pixels; each covers all BR rows
@@ -2122,6 +2123,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const uint32_t lds0 = lds_addr_of(lds);
   const int wr = wave >> 2, wp = wave & 3;   // row group (WRW = 2), pixel group
+  if (WRW == 2 && a.prio_hi && wave >= 4) __builtin_amdgcn_s_setprio(1);
   int bid;
   {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one walker
     const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
