@@ -948,7 +948,7 @@ def test_run_unet_batch_equals_per_photo_calls():
 
 @pytest.mark.parametrize("dtype", ["fp32", "mixed", "bf16"])
 def test_small_batch_split_k_plan(dtype, monkeypatch):
-    """The small-batch plan (csrc/unet_capi.cpp layer_ksplit: the deep layers whose tile grid under-fills
+    """The small-batch plan (csrc/unet_capi.cpp layer_split: the deep layers whose tile grid under-fills
     the 256 CUs at N <= 4 run as K slices into fp32 partials + a slice-ordered reduction): engaged at
     N = 1 (its partial buffer enlarges the workspace), bitwise repeatable, bitwise the same image at N =
     1, 3 and 4 (the slice counts depend on the layer only), pinned to the reference masks and logits of

@@ -130,7 +130,7 @@ struct unet_handle {
   bool capturing = false;        // inside unet_graph_create: no event record / wait in the stream
   void* comm = nullptr;          // RCCL communicator (unet_comm_init), ncclComm_t
   unsigned long long generation = 1;   // bumped whenever device pointers a graph captured change
-  // split-K of under-filled layers (small batches, layer_ksplit): the largest slice count
+  // split-K of under-filled layers (small batches, layer_split): the largest slice count
   // (UNET_MI355X_KSPLIT; 0 or 1 = never split) and per-launch forced counts for A/B runs
   // (UNET_MI355X_KSPLIT_FORCE="i:ks,...", i = 3x3 layer 0..16 or 17 + ConvTranspose 0..3; 0 = auto)
   int ksplit_max = 32;
@@ -219,29 +219,47 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // LDS-halo family (fp32 plan, 3x3 and ConvTranspose) with a plain store, pool or scatter epilogue;
 // never the fused first conv, the head or the fused up1.
 constexpr int kSmallBatch = 4;
-int layer_ksplit(const unet_handle* h, int id, const Layer& L, int epi, int N, int Hl, int Wl) {
-  if (h->ksplit_max <= 1 || N <= 0 || N > kSmallBatch || Hl <= 0 || Wl <= 0) return 1;
+struct Split {
+  int ks = 1;     // K slices (1 = the layer runs unsplit)
+  int rows = 0;   // 8-wave ring: row tile of the slices (64 = halves of the 128-row packing), 0 = the layer's own
+};
+Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, int Hl, int Wl) {
+  Split best;
+  if (h->ksplit_max <= 1 || N <= 0 || N > kSmallBatch || Hl <= 0 || Wl <= 0) return best;
   const bool ring8 = L.cfg == CFG_RING8_R128 && L.dt != DType::F32 && L.taps == 9;
   const bool halo = cfg_is_halo(L.cfg) && L.dt == DType::F32;
-  if (!(ring8 || halo)) return 1;
-  if (!(epi == EPI_STORE || epi == EPI_POOL || epi == EPI_UPSCATTER)) return 1;
+  if (!(ring8 || halo)) return best;
+  if (!(epi == EPI_STORE || epi == EPI_POOL || epi == EPI_UPSCATTER)) return best;
   const int chunk = 32;   // K slice granule: one 32-channel chunk (ring8 16-bit, halo fp32)
   const int nch = L.cin / chunk;
-  if (L.cin % chunk) return 1;
+  if (L.cin % chunk) return best;
   const int tw = cfg_tile_w(L.cfg), th = cfg_tile_h(L.cfg);
-  // blocks of ONE image (the plan depends on the layer and resolution only, not on N)
-  const long long blocks = (long long)(L.ctot / cfg_rows(L.cfg)) * ((Hl + th - 1) / th) * ((Wl + tw - 1) / tw);
   const int cap = ring8 ? 256 : 512;   // resident blocks: one 512-thread ring block / two halo blocks per CU
-  const double rate = ring8 ? 5.5e12 : 0.55e12, bw = 5e12, t_launch = 4e-6;   // per-CU FLOP/s, B/s
+  // per-CU FLOP/s of the family and the partials' effective write + read rate, fitted to the batch-1
+  // per-layer times with and without the split (profiles/tune_r4b_bs1_ksplit_*.txt: 134 MB of fp32
+  // partials cost ~42 us = 3.2 TB/s including the reduction's launch)
+  const double bw = 3.2e12, t_launch = 4e-6;
   const double P = (double)Hl * Wl;
   const double flops = 2.0 * L.ctot * L.cin * L.taps * P;
+  // blocks of ONE image (the plan depends on the layer and resolution only, not on N)
+  const long long tiles = (long long)((Hl + th - 1) / th) * ((Wl + tw - 1) / tw);
   const int forced = h->ksplit_force[id];
-  if (forced > 0) return (forced <= nch && nch % forced == 0 && blocks * forced <= 8LL * cap) ? forced : 1;
-  int best = 1;
-  double tbest = flops / ((double)std::min<long long>(blocks, 256) * rate);
-  for (int ks = 2; ks <= h->ksplit_max && nch % ks == 0 && nch / ks >= (ring8 ? 2 : 1) && blocks * ks <= cap; ks *= 2) {
-    const double t = flops / ((double)std::min<long long>(blocks * ks, 256) * rate) + ks * P * L.ctot * 8.0 / bw + t_launch;
-    if (t < tbest) { tbest = t; best = ks; }
+  // candidate row tiles: the layer's own; on the ring also 64-row halves (twice the blocks per slice, so
+  // half the slices for the same CU count; 0.8x the per-CU rate: half the MFMAs per halo byte)
+  const int own = cfg_rows(L.cfg);
+  double tbest = flops / ((double)std::min<long long>(tiles * (L.ctot / own), 256) * (ring8 ? 6e12 : 0.5e12));
+  for (int rows : {own, ring8 ? 64 : 0}) {
+    if (rows == 0) break;
+    const double rate = ring8 ? (rows == 128 ? 6e12 : 4.8e12) : 0.5e12;
+    const long long blocks = tiles * (L.ctot / rows);
+    if (forced > 0) {   // A/B runs: the forced slice count on the layer's own row tile
+      if (rows == own && forced <= nch && nch % forced == 0 && blocks * forced <= 8LL * cap) best = {forced, 0};
+      continue;
+    }
+    for (int ks = 2; ks <= h->ksplit_max && nch % ks == 0 && nch / ks >= (ring8 ? 2 : 1) && blocks * ks <= cap; ks *= 2) {
+      const double t = flops / ((double)std::min<long long>(blocks * ks, 256) * rate) + ks * P * L.ctot * 8.0 / bw + t_launch;
+      if (t < 0.9 * tbest) { tbest = t; best = {ks, rows == own ? 0 : rows}; }   // a split must win by 10 %
+    }
   }
   return best;
 }
@@ -252,7 +270,7 @@ size_t split_bytes(const unet_handle* h, int N, int H, int W) {
   size_t m = 0;
   auto one = [&](int id, const Layer& L, int epi, int lvl) {
     const int Hl = H >> lvl, Wl = W >> lvl;
-    const int ks = layer_ksplit(h, id, L, epi, N, Hl, Wl);
+    const int ks = layer_split(h, id, L, epi, N, Hl, Wl).ks;
     if (ks > 1) m = std::max(m, (size_t)ks * N * Hl * Wl * L.ctot * 4);
   };
   for (int i = 0; i < 17; ++i) {
@@ -981,10 +999,14 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   const int id = (&L >= h->L && &L < h->L + 17) ? (int)(&L - h->L) : 17 + (int)(&L - h->U);
   a.xcd_rows = id < 17 ? (int)((h->xcd_rows >> id) & 1u) : 0;
   a.prio_hi = h->prio_hi;
-  const int ks = layer_ksplit(h, id, L, epi, N, H, W);
-  if (ks > 1) {   // small-batch plan: K slices into fp32 partials, then the layer's epilogue over their sum
+  const Split sp = layer_split(h, id, L, epi, N, H, W);
+  if (sp.ks > 1) {   // small-batch plan: K slices into fp32 partials, then the layer's epilogue over their sum
     a.part = static_cast<float*>(h->part);
-    a.ksplit = ks;
+    a.ksplit = sp.ks;
+    if (sp.rows) {   // finer row tiles over the layer's own packing (8-wave ring)
+      a.src_br = cfg_rows(L.cfg);
+      a.n_ct = L.ctot / sp.rows;
+    }
     hipError_t e = launch_igemm(L.dt, L.dt, L.dt, L.cfg, L.taps, EPI_PARTIAL, a, s);
     if (e == hipSuccess) e = launch_splitk_reduce(L.dto, epi == EPI_POOL ? L.dtq : L.dto, epi, a, s);
     if (e != hipSuccess) return fail(UNET_EHIP, std::string("split-K igemm launch: ") + hipGetErrorString(e));
@@ -1025,7 +1047,7 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
 
   int li = 0;
   auto mark = [&]() { if (ev) (void)hipEventRecord(ev[li], s); ++li; };
-  h->part = buf(B.part);   // split-K partials of the small-batch plan (run_igemm, layer_ksplit)
+  h->part = buf(B.part);   // split-K partials of the small-batch plan (run_igemm, layer_split)
   mark();
   // down1.net.0 (C -> 64): fused into down1.3 on the 16-bit ring path (fed by the pre-cast input),
   // a direct conv otherwise

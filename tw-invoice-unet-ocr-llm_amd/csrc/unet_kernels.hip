@@ -219,6 +219,25 @@ __device__ __forceinline__ void glds16_s(const void* src, uint32_t lds_addr) {
       : "=&s"(keep)
       : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_addr)));
 }
+// The saddr form: lane l's 16 bytes come from sbase + voff, a wave-uniform 64-bit base in SGPRs plus a
+// 32-bit per-lane offset.  A stream whose per-lane pattern is fixed (the packed weight pieces) then
+// advances by scalar adds only, instead of a 64-bit VALU add per piece (round 4).
+__device__ __forceinline__ void glds16_sv(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+  const uintptr_t u = reinterpret_cast<uintptr_t>(sbase);
+  // (readfirstlane returns int: each half goes through uint32_t, so the low half is not sign-extended)
+  const unsigned long long ub =
+      ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(u >> 32)) << 32) |
+      (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)u);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(ub), "s"(__builtin_amdgcn_readfirstlane(lds_addr)));
+}
 // LDS address of a __shared__ object (a constant for the kernel's one LDS array)
 __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
   return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_t)p));
@@ -1562,8 +1581,15 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 
   // weights of row tile ct in step order (the 4-wave ring's packing): piece j of a step = rows
   // 16j .. 16j+15; per lane one 16-byte chunk of row 16j + lane/4 at position chunk ^ ((row>>1)&3)
-  const char* wblk = reinterpret_cast<const char*>(a.wgt) + ((size_t)ct * ST * KS + (size_t)kslice * S) * SLOT +
-                     (lane >> 2) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
+  // (the row tile's base is wave-uniform: the DMA takes it in SGPRs and the lane's 16-byte chunk as a
+  // 32-bit offset, glds16_sv)
+  // EPI_PARTIAL on a finer row tile than the packing's (a.src_br = 128 with BR = 64: the batch-1 split
+  // gets twice the blocks per K slice, so half the slices -- and half the fp32 partials -- for the same
+  // CU count): row tile ct is part ct % R of packed row tile ct / R, whose steps are R times longer
+  const int R = (PART && a.src_br > BR) ? a.src_br / BR : 1;
+  const char* wblk = reinterpret_cast<const char*>(a.wgt) + ((size_t)(ct / R) * ST * KS + (size_t)kslice * S) * SLOT * R +
+                     (size_t)(ct % R) * WSLOT;
+  const uint32_t wlane = (lane >> 2) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
   const char* in = reinterpret_cast<const char*>(a.in);
   const char* zero = reinterpret_cast<const char*>(a.zero);
 
@@ -1603,14 +1629,17 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   };
   // weights of step s into LDS slot `dst_slot` (this wave's pieces)
   auto issue_w_step = [&](int s, int dst_slot) {
-    const char* src = wblk + (size_t)s * SLOT;
+    const char* src = wblk + (size_t)s * SLOT * R;
     const uint32_t dst = lds0 + WOFF + dst_slot * SLOT;
 #pragma unroll
     for (int k = 0; k < (PIECES + NW - 1) / NW; ++k) {
       const int j = wave + k * NW;
+      // piece j = 16 rows of tap j / PPT (PPT = pieces per tap); with R > 1 the packed taps are R times apart
+      constexpr int PPT = WSLOT / 1024;
+      const int off = PART ? (j / PPT) * WSLOT * R + (j % PPT) * 1024 : j * 1024;
       // wave-uniform; no test at all when every wave has the same count (straight-line issue: the
       // compiler had moved the tested pieces out of line, a taken branch each)
-      if (PIECES % NW == 0 || j < PIECES) glds16_s(src + j * 1024, dst + j * 1024);
+      if (PIECES % NW == 0 || j < PIECES) glds16_sv(src + off, wlane, dst + j * 1024);
     }
   };
   int wq_s = 0, wq_slot = 0;
@@ -2082,6 +2111,7 @@ static hipError_t launch_ring8(const IgemmArgs& a, hipStream_t s) {
   if (WST && (9 / TPS) * (a.Cin / G::BKE) > G::WST_STEPS) return hipErrorInvalidValue;
   const int KS = EPI == EPI_PARTIAL ? a.ksplit : 1;
   if (KS < 1 || a.Cin % (G::BKE * KS) || (EPI == EPI_PARTIAL && !a.part)) return hipErrorInvalidValue;
+  if (a.src_br && (EPI != EPI_PARTIAL || a.src_br % G::BR || a.Ctot % a.src_br)) return hipErrorInvalidValue;
   const int n_mt = a.N * a.tiles_y * a.tiles_x * KS;   // items: (pixel tile, K slice)
   int n_slots = kNumCUs / a.n_ct;   // one 512-thread block per CU
   n_slots -= n_slots % KS;          // every walker keeps one K slice (n_mt is a multiple of KS)
@@ -2140,8 +2170,8 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
   const int S = a.Cin / BKE;
   const int total = items * S;
 
-  const char* wblk = reinterpret_cast<const char*>(a.wgt) +
-                     (wave * WI * 16 + (lane >> 2)) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
+  const char* wblk = reinterpret_cast<const char*>(a.wgt) + wave * WI * 16 * 64;   // wave-uniform (glds16_sv)
+  const uint32_t wlane = (lane >> 2) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
   const char* in = reinterpret_cast<const char*>(a.in);
   const char* zero = reinterpret_cast<const char*>(a.zero);
   auto tile_of = [&](int i, int& n, int& ty, int& tx) {
@@ -2162,7 +2192,7 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
     const uint32_t As = lds0 + iss_slot * SLOT;
 #pragma unroll
     for (int j = 0; j < WI; ++j)
-      glds16_s(wct + (size_t)iss_c * ASLOT + j * 1024, As + (wave * WI + j) * 1024);
+      glds16_sv(wct + (size_t)iss_c * ASLOT + j * 1024, wlane, As + (wave * WI + j) * 1024);
     if (iss_c == 0) {
       int n, ty, tx;
       tile_of(iss_i, n, ty, tx);
@@ -2456,7 +2486,12 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
         case CFG_HALO_R64_W4: if constexpr (sizeof(T) == 4) return launch_halo<T, 1, 4, 4, 3, EPI, 3>(a, s); break;
         case CFG_HALO_R64_W8: if constexpr (sizeof(T) == 4) return launch_halo<T, 1, 8, 4, 3, EPI, 3>(a, s); break;
         case CFG_HALO_R128: if constexpr (sizeof(T) == 4) return launch_halo<T, 1, 4, 8, 2, EPI, 3>(a, s); break;
-        case CFG_RING8_R128: if constexpr (sizeof(T) == 2) return launch_ring8<T, 8, 3, EPI, 3, 0, T, T>(a, s); break;
+        case CFG_RING8_R128:   // 128-row tiles, or 64-row tiles over the 128-row packing (a.src_br)
+          if constexpr (sizeof(T) == 2) {
+            if (a.src_br == 128) return launch_ring8<T, 4, 3, EPI, 3, 0, T, T>(a, s);
+            return launch_ring8<T, 8, 3, EPI, 3, 0, T, T>(a, s);
+          }
+          break;
         default: break;
       }
     }
@@ -2884,9 +2919,17 @@ __global__ __launch_bounds__(256) void x_to_px4_kernel(const void* __restrict__ 
   }
 }
 
+// Grid-stride element kernels: at most 4096 blocks, and no more than one block per 1024 pixels (a
+// batch-1 512^2 input is 256 blocks: the fixed 4096-block grid took 33 us there, mostly dispatching
+// blocks with nothing to do).
+static dim3 elem_grid(long long pixels) {
+  const long long b = (pixels + 1023) / 1024;
+  return dim3((unsigned)(b < 1 ? 1 : (b > 4096 ? 4096 : b)));
+}
+
 hipError_t launch_x_to_px4(DType t, const void* x, int layout, int xdt, int N, int C, int H, int W, void* out,
                            hipStream_t s) {
-  const dim3 grid(4096), block(256);
+  const dim3 grid = elem_grid((long long)N * H * W), block(256);
   if (t == DType::BF16)
     hipLaunchKernelGGL(x_to_px4_kernel<__bf16>, grid, block, 0, s, x, layout, xdt, N, C, H, W, static_cast<__bf16*>(out));
   else if (t == DType::F16)
@@ -2908,7 +2951,7 @@ __global__ __launch_bounds__(256) void x_to_nchw_f32_kernel(const void* __restri
 
 hipError_t launch_x_to_nchw_f32(const void* x, int layout, int xdt, int N, int C, int H, int W, float* out,
                                 hipStream_t s) {
-  hipLaunchKernelGGL(x_to_nchw_f32_kernel, dim3(4096), dim3(256), 0, s, x, layout, xdt, N, C, H, W, out);
+  hipLaunchKernelGGL(x_to_nchw_f32_kernel, elem_grid((long long)N * H * W), dim3(256), 0, s, x, layout, xdt, N, C, H, W, out);
   return hipGetLastError();
 }
 
