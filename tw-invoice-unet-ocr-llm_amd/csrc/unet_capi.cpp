@@ -256,6 +256,10 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
       if (rows == own && forced <= nch && nch % forced == 0 && blocks * forced <= 8LL * cap) best = {forced, 0};
       continue;
     }
+    if (rows != own && epi != EPI_UPSCATTER) {   // finer row tiles alone, no K split (no partials)
+      const double t = flops / ((double)std::min<long long>(blocks, 256) * rate);
+      if (t < 0.9 * tbest) { tbest = t; best = {1, rows}; }
+    }
     for (int ks = 2; ks <= h->ksplit_max && nch % ks == 0 && nch / ks >= (ring8 ? 2 : 1) && blocks * ks <= cap; ks *= 2) {
       const double t = flops / ((double)std::min<long long>(blocks * ks, 256) * rate) + ks * P * L.ctot * 8.0 / bw + t_launch;
       if (t < 0.9 * tbest) { tbest = t; best = {ks, rows == own ? 0 : rows}; }   // a split must win by 10 %
@@ -1000,6 +1004,10 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.xcd_rows = id < 17 ? (int)((h->xcd_rows >> id) & 1u) : 0;
   a.prio_hi = h->prio_hi;
   const Split sp = layer_split(h, id, L, epi, N, H, W);
+  if (sp.ks == 1 && sp.rows) {   // small-batch plan, unsplit: finer row tiles over the layer's packing
+    a.src_br = cfg_rows(L.cfg);
+    a.n_ct = L.ctot / sp.rows;
+  }
   if (sp.ks > 1) {   // small-batch plan: K slices into fp32 partials, then the layer's epilogue over their sum
     a.part = static_cast<float*>(h->part);
     a.ksplit = sp.ks;

@@ -1586,7 +1586,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   // EPI_PARTIAL on a finer row tile than the packing's (a.src_br = 128 with BR = 64: the batch-1 split
   // gets twice the blocks per K slice, so half the slices -- and half the fp32 partials -- for the same
   // CU count): row tile ct is part ct % R of packed row tile ct / R, whose steps are R times longer
-  const int R = (PART && a.src_br > BR) ? a.src_br / BR : 1;
+  // (also unsplit: the batch-1 plan runs under-filled 128-row layers on 64-row tiles, FINE instantiations)
+  constexpr bool FINE = TCW == 4 && NS == 3 && TPS == 3 && WST == 0 && HS == 0 && !UPF;
+  const int R = ((PART || FINE) && a.src_br > BR) ? a.src_br / BR : 1;
   const char* wblk = reinterpret_cast<const char*>(a.wgt) + ((size_t)(ct / R) * ST * KS + (size_t)kslice * S) * SLOT * R +
                      (size_t)(ct % R) * WSLOT;
   const uint32_t wlane = (lane >> 2) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
@@ -1636,7 +1638,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       const int j = wave + k * NW;
       // piece j = 16 rows of tap j / PPT (PPT = pieces per tap); with R > 1 the packed taps are R times apart
       constexpr int PPT = WSLOT / 1024;
-      const int off = PART ? (j / PPT) * WSLOT * R + (j % PPT) * 1024 : j * 1024;
+      const int off = (PART || FINE) ? (j / PPT) * WSLOT * R + (j % PPT) * 1024 : j * 1024;
       // wave-uniform; no test at all when every wave has the same count (straight-line issue: the
       // compiler had moved the tested pieces out of line, a taken branch each)
       if (PIECES % NW == 0 || j < PIECES) glds16_sv(src + off, wlane, dst + j * 1024);
@@ -2111,7 +2113,8 @@ static hipError_t launch_ring8(const IgemmArgs& a, hipStream_t s) {
   if (WST && (9 / TPS) * (a.Cin / G::BKE) > G::WST_STEPS) return hipErrorInvalidValue;
   const int KS = EPI == EPI_PARTIAL ? a.ksplit : 1;
   if (KS < 1 || a.Cin % (G::BKE * KS) || (EPI == EPI_PARTIAL && !a.part)) return hipErrorInvalidValue;
-  if (a.src_br && (EPI != EPI_PARTIAL || a.src_br % G::BR || a.Ctot % a.src_br)) return hipErrorInvalidValue;
+  constexpr bool fine = TCW == 4 && NS == 3 && TPS == 3 && WST == 0 && HS == 0 && EPI != EPI_UPFUSE;
+  if (a.src_br && (!(EPI == EPI_PARTIAL || fine) || a.src_br % G::BR || a.Ctot % a.src_br)) return hipErrorInvalidValue;
   const int n_mt = a.N * a.tiles_y * a.tiles_x * KS;   // items: (pixel tile, K slice)
   int n_slots = kNumCUs / a.n_ct;   // one 512-thread block per CU
   n_slots -= n_slots % KS;          // every walker keeps one K slice (n_mt is a multiple of KS)
@@ -2535,7 +2538,12 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
     case CFG_RING_FUSED_IN:
       if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
       break;
-    case CFG_RING8_R128: if constexpr (EPI != EPI_HEAD) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ>(a, s); break;
+    case CFG_RING8_R128:   // (a.src_br = 128: the batch-1 plan's 64-row tiles over the 128-row packing)
+      if constexpr (EPI != EPI_HEAD) {
+        if (a.src_br == 128) return launch_ring8<T, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
+        return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ>(a, s);
+      }
+      break;
     case CFG_RING8_R64_T9: if constexpr (EPI != EPI_PARTIAL) return launch_ring8<T, 4, 2, EPI, 9, 0, TO, TQ>(a, s); break;
     case CFG_RING8_R64_WS: return launch_ring8<T, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
     case CFG_RING8_FUSED_IN:
