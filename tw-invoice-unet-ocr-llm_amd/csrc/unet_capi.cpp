@@ -137,6 +137,7 @@ struct unet_handle {
   int ksplit_force[21] = {};
   unsigned xcd_rows = 0;   // bit i: 3x3 layer i walks with XCD-owned row tiles (UNET_MI355X_XCDROWS="i,...")
   int prio_hi = 0;         // UNET_MI355X_PRIO=1: waves 4-7 of the 8-wave kernels at s_setprio 1 (A/B option)
+  int convt_ws = 1;        // ConvTranspose with Cin <= 256 on the weight-stationary kernel (UNET_MI355X_CONVT_WS=0: off)
   void* part = nullptr;   // the current forward's partial buffer (workspace region Buffers::part)
 };
 
@@ -228,6 +229,14 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
   if (h->ksplit_max <= 1 || N <= 0 || N > kSmallBatch || Hl <= 0 || Wl <= 0) return best;
   const bool ring8 = L.cfg == CFG_RING8_R128 && L.dt != DType::F32 && L.taps == 9;
   const bool halo = cfg_is_halo(L.cfg) && L.dt == DType::F32;
+  if (L.cfg == CFG_TRING_R256 && L.dt != DType::F32 && epi == EPI_UPSCATTER) {
+    // the 16-bit ConvTranspose ring: no K split (its partials' bytes per FLOP are 4-8x a 3x3 layer's),
+    // but 128-row tiles over the 256-row packing (4-wave blocks, two per CU) when its 256-row grid
+    // fills less than half the CUs (batch 1: up4 32 blocks, up3 64, up2 128)
+    const long long blocks = (long long)(L.ctot / 256) * ((Hl + 15) / 16) * ((Wl + 15) / 16);
+    if (blocks < 128 && L.ctot % 256 == 0) best.rows = 128;
+    return best;
+  }
   if (!(ring8 || halo)) return best;
   if (!(epi == EPI_STORE || epi == EPI_POOL || epi == EPI_UPSCATTER)) return best;
   const int chunk = 32;   // K slice granule: one 32-channel chunk (ring8 16-bit, halo fp32)
@@ -589,10 +598,12 @@ int check_geometry(const unet_handle* h, int N, int H, int W) {
 const char* tname(DType t) { return t == DType::F32 ? "float" : t == DType::BF16 ? "__bf16" : "_Float16"; }
 
 // "kernel<template args>" of a layer, in the same spelling as the demangled symbol
-std::string layer_label(const Layer& L, int epi) {
+std::string layer_label(const unet_handle* h, const Layer& L, int epi) {
   char buf[160];
   const int cfg = L.cfg;
-  if (cfg_is_tring(cfg)) {
+  if (cfg == CFG_TRING_R256 && h->convt_ws && L.dt != DType::F32 && L.cin <= 256) {   // launch_up: Cin <= 8 steps
+    std::snprintf(buf, sizeof buf, "convT_ws_kernel<%s, %s>", tname(L.dt), tname(L.dto));
+  } else if (cfg_is_tring(cfg)) {
     std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, %d, %d, %s>", tname(L.dt), cfg == CFG_TRING_R256 ? 4 : 3,
                   cfg == CFG_TRING_R256 ? 2 : 1, tname(L.dto));
   } else if (cfg_is_ring8(cfg)) {
@@ -629,12 +640,12 @@ void build_labels(unet_handle* h) {
       continue;
     }
     if (id >= 100) {   // a fused up1 launches nothing: empty label (tools: its time and work go to conv2.3)
-      h->labels[i] = (id == 103 && h->fuse_up1) ? std::string() : layer_label(h->U[id - 100], EPI_UPSCATTER);
+      h->labels[i] = (id == 103 && h->fuse_up1) ? std::string() : layer_label(h, h->U[id - 100], EPI_UPSCATTER);
       continue;
     }
     int epi = id == C1B ? EPI_HEAD : (id == D1B || id == D2B || id == D3B || id == D4B) ? EPI_POOL : EPI_STORE;
     if (id == C2B && h->fuse_up1) epi = EPI_UPFUSE;
-    h->labels[i] = layer_label(h->L[id], epi);
+    h->labels[i] = layer_label(h, h->L[id], epi);
   }
 }
 
@@ -799,6 +810,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   }
   if (const char* ks = std::getenv("UNET_MI355X_KSPLIT")) h->ksplit_max = std::atoi(ks);
   if (const char* pr = std::getenv("UNET_MI355X_PRIO")) h->prio_hi = std::atoi(pr) != 0;
+  if (const char* cw = std::getenv("UNET_MI355X_CONVT_WS")) h->convt_ws = std::atoi(cw) != 0;
   if (const char* xr = std::getenv("UNET_MI355X_XCDROWS")) {   // "i,j,..." 3x3 layer indices (A/B runs)
     for (const char* p = xr; *p;) {
       const int li = std::atoi(p);
@@ -1003,10 +1015,13 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   const int id = (&L >= h->L && &L < h->L + 17) ? (int)(&L - h->L) : 17 + (int)(&L - h->U);
   a.xcd_rows = id < 17 ? (int)((h->xcd_rows >> id) & 1u) : 0;
   a.prio_hi = h->prio_hi;
+  a.convt_ws = h->convt_ws;
   const Split sp = layer_split(h, id, L, epi, N, H, W);
+  int cfg = L.cfg;
   if (sp.ks == 1 && sp.rows) {   // small-batch plan, unsplit: finer row tiles over the layer's packing
     a.src_br = cfg_rows(L.cfg);
     a.n_ct = L.ctot / sp.rows;
+    if (L.cfg == CFG_TRING_R256) cfg = CFG_TRING_R128;   // the 4-wave 128-row ConvTranspose ring
   }
   if (sp.ks > 1) {   // small-batch plan: K slices into fp32 partials, then the layer's epilogue over their sum
     a.part = static_cast<float*>(h->part);
@@ -1020,7 +1035,7 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
     if (e != hipSuccess) return fail(UNET_EHIP, std::string("split-K igemm launch: ") + hipGetErrorString(e));
     return UNET_OK;
   }
-  hipError_t e = launch_igemm(L.dt, L.dto, epi == EPI_POOL ? L.dtq : L.dto, L.cfg, L.taps, epi, a, s);
+  hipError_t e = launch_igemm(L.dt, L.dto, epi == EPI_POOL ? L.dtq : L.dto, cfg, L.taps, epi, a, s);
   if (e != hipSuccess) return fail(UNET_EHIP, std::string("igemm launch: ") + hipGetErrorString(e));
   return UNET_OK;
 }

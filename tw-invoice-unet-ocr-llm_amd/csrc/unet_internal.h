@@ -64,6 +64,7 @@ struct IgemmArgs {
   float* part;
   int ksplit;
   int src_br;   // EPI_PARTIAL on the 8-wave ring: row tile of the weight packing when finer than BR (0 = BR)
+  int convt_ws; // ConvTranspose on CFG_TRING_R256 with Cin <= 256: the weight-stationary kernel (convT_ws_kernel)
   // 8-wave ring: blocks of one XCD share row tiles (ct = XCD label mod n_ct) instead of pixel tiles,
   // so an XCD's L2 holds 1/min(8, n_ct) of the layer's weights (and streams every pixel tile's halo)
   int xcd_rows;

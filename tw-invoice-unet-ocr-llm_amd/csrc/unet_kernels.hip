@@ -2190,12 +2190,15 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
   // pixels outside the image -- 4 KB, so + c * 64 stays inside it), every step adds c * 64.
   int iss_c = 0, iss_i = 0, iss_slot = 0;
   const char* bsrc[BI];
-  const char* wct = wblk + (size_t)ct * S * ASLOT;
+  // (batch-1 plan: 128-row tiles over the 256-row packing, a.src_br = 256 -- row tile ct is half ct % R of
+  // packed row tile ct / R, whose steps are R times longer)
+  const int R = (WRW == 1 && a.src_br > BR) ? a.src_br / BR : 1;
+  const char* wct = wblk + (size_t)(ct / R) * S * ASLOT * R + (size_t)(ct % R) * ASLOT;
   auto issue = [&]() {
     const uint32_t As = lds0 + iss_slot * SLOT;
 #pragma unroll
     for (int j = 0; j < WI; ++j)
-      glds16_sv(wct + (size_t)iss_c * ASLOT + j * 1024, wlane, As + (wave * WI + j) * 1024);
+      glds16_sv(wct + (size_t)iss_c * ASLOT * R + j * 1024, wlane, As + (wave * WI + j) * 1024);
     if (iss_c == 0) {
       int n, ty, tx;
       tile_of(iss_i, n, ty, tx);
@@ -2296,6 +2299,160 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
       ++item;
     }
   }
+}
+
+// ConvTranspose2d with the row tile's weights resident in LDS (weight-stationary, round 4): for
+// Cin <= 256 (up2; up1 when it is not fused into conv2.3) the 256-row tile's whole K -- at most 8
+// steps x 16 KB -- fits beside a two-slot pixel ring (2 x 16 KB; 160 KiB in all), so only the input
+// pixels stream: 16 KB of LDS-DMA per step instead of the both-streamed ring's 32 KB.  That ring
+// moves ~32 GB/s per CU of loads + scatter stores on up2 (MFMA 28-33 % busy, HBM 4.3 TB/s), the
+// per-CU LDS-DMA rate the guide measures (MI355X_MICROARCH 'ldsdma-fill').  Same tile, K order,
+// fragment layouts and swizzles as convT_ring_kernel<T, 8, 4, 2>, accumulators starting at the bias
+// (held in registers here: the LDS is full), so the two agree bit for bit.  One step of DMA cover:
+// the next step's pixels are issued under the current step's first MFMAs.
+template <typename T, typename TO>
+__global__ __launch_bounds__(512, 1) void convT_ws_kernel(const IgemmArgs a) {
+  constexpr int NW = 8, TC = 8, TP = 4, BR = 256, BKE = 64 / (int)sizeof(T), SMAX = 8;
+  constexpr int WI = BR / (16 * NW);          // A DMA instructions per wave and step (prologue only)
+  constexpr int BI = 256 / (16 * NW);         // B DMA instructions per wave and step
+  constexpr int ASTEP = BR * 64, BSLOT = 256 * 64, BOFF = SMAX * ASTEP;
+  __shared__ __attribute__((aligned(16))) char lds[BOFF + 2 * BSLOT];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const uint32_t lds0 = lds_addr_of(lds);
+  const int wr = wave >> 2, wp = wave & 3;   // row group, pixel group
+  int bid;
+  {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one walker
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
+    const int b = blockIdx.x, x = b & 7, k = b >> 3;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  }
+  const int ct = bid % a.n_ct;
+  const int slot = bid / a.n_ct;
+  const int n_slots = gridDim.x / a.n_ct;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  if (slot >= n_mt) return;
+  const int items = (n_mt - slot + n_slots - 1) / n_slots;
+  const int H = a.H, W = a.W;
+  const int S = a.Cin / BKE;                  // <= SMAX (launcher)
+  const int total = items * S;
+  const char* in = reinterpret_cast<const char*>(a.in);
+  const char* zero = reinterpret_cast<const char*>(a.zero);
+  auto tile_of = [&](int i, int& n, int& ty, int& tx) {
+    int mt = slot + i * n_slots;
+    tx = mt % a.tiles_x;
+    mt /= a.tiles_x;
+    ty = mt % a.tiles_y;
+    n = mt / a.tiles_y;
+  };
+  // prologue: the row tile's weights, all S steps (the ring kernel's packing, [ct][s][256 rows][64 B])
+  {
+    const char* wct = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * ASTEP + wave * WI * 1024;
+    const uint32_t wlane = (lane >> 2) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
+    for (int st = 0; st < S; ++st)
+#pragma unroll
+      for (int j = 0; j < WI; ++j)
+        glds16_sv(wct + (size_t)st * ASTEP + j * 1024, wlane, lds0 + st * ASTEP + (wave * WI + j) * 1024);
+  }
+  // pixel stream: per-lane pointers set at a tile's first step (the zero page for pixels outside the
+  // image), + c * 64 B per step, as in convT_ring_kernel
+  int iss_c = 0, iss_i = 0, iss_slot = 0;
+  const char* bsrc[BI];
+  auto issue_b = [&]() {
+    if (iss_c == 0) {
+      int n, ty, tx;
+      tile_of(iss_i, n, ty, tx);
+#pragma unroll
+      for (int j = 0; j < BI; ++j) {
+        const int r = (wave * BI + j) * 16 + (lane >> 2), py = r >> 4, px = r & 15;
+        const int iy = ty * 16 + py, ix = tx * 16 + px;
+        const int chk = ((lane & 3) ^ ((py & 1) << 1)) << 4;
+        const bool ok = iy < H && ix < W;
+        bsrc[j] = ok ? in + ((long long)(n * H + iy) * W + ix) * a.ldi * (long long)sizeof(T) + chk : zero + chk;
+      }
+    }
+    const uint32_t Bs = lds0 + BOFF + iss_slot * BSLOT;
+#pragma unroll
+    for (int j = 0; j < BI; ++j) glds16_s(bsrc[j] + iss_c * BKE * (int)sizeof(T), Bs + (wave * BI + j) * 1024);
+    iss_slot ^= 1;
+    if (++iss_c == S) { iss_c = 0; ++iss_i; }
+  };
+  issue_b();
+  // the accumulators start at the bias: the lane's rows wr*128 + 64 (t / 4) + 16 q + 4 (t % 4) + e
+  const int col = lane & 15, q = lane >> 4;
+  f32x4 bv[TC];
+#pragma unroll
+  for (int t = 0; t < TC; ++t)
+    bv[t] = *reinterpret_cast<const f32x4*>(a.bias + ct * BR + wr * 16 * TC + 64 * (t / 4) + 16 * q + 4 * (t % 4));
+  f32x4 acc[TC][TP];
+  auto init_acc = [&]() {
+#pragma unroll
+    for (int t = 0; t < TC; ++t)
+#pragma unroll
+      for (int p = 0; p < TP; ++p) acc[t][p] = bv[t];
+  };
+  init_acc();
+  int prow[TP];
+#pragma unroll
+  for (int p = 0; p < TP; ++p) {
+    int py, px;
+    pix_of((wp * TP + p) * 16 + col, py, px);
+    prow[p] = (py * 16 + px) * 64 + ((q ^ ((py & 1) << 1)) << 4);
+  }
+  const int wrow = (wr * 16 * TC + col) * 64 + ((q ^ ((col >> 1) & 3)) << 4);
+  wait_vm_barrier<0>();   // weights and step 0's pixels landed (the bias loads too)
+
+  int c = 0, item = 0;
+  for (int g = 0; g < total; ++g) {
+    const bool dma = g + 1 < total;
+    const char* As = lds + c * ASTEP + wrow;
+    const char* Bs = lds + BOFF + (g & 1) * BSLOT;
+    frag_t bq[TP], ar[3];
+#pragma unroll
+    for (int p = 0; p < TP; ++p) bq[p] = *reinterpret_cast<const frag_t*>(Bs + prow[p]);
+    ar[0] = *reinterpret_cast<const frag_t*>(As);
+    ar[1] = *reinterpret_cast<const frag_t*>(As + 16 * 64);
+    __builtin_amdgcn_sched_group_barrier(0x100, TP + 2, 0);
+#pragma unroll
+    for (int t = 0; t < TC; ++t) {
+      if (t + 2 < TC) ar[(t + 2) % 3] = *reinterpret_cast<const frag_t*>(As + (t + 2) * 16 * 64);
+      const frag_t af = ar[t % 3];
+#pragma unroll
+      for (int p = 0; p < TP; ++p)
+        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
+      if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+      // the next step's pixels into the other slot (its last reads were the previous step's, behind
+      // the previous barrier), under this step's first MFMAs
+      if (t == 1 && dma) issue_b();
+    }
+    // step g+1's pixels landed (the only load in flight; older scatter stores are waited for too)
+    wait_vm_barrier<0>();
+    if (++c == S) {
+      c = 0;
+      int n, ty, tx;
+      tile_of(item, n, ty, tx);
+#pragma unroll
+      for (int h = 0; h < TC / 4; ++h)
+        conv_epilogue<TO, TO, TP, EPI_UPSCATTER, 16, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n,
+                                                         ty * 16, tx * 16, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
+                                                         nullptr, nullptr, nullptr);
+      init_acc();
+      ++item;
+    }
+  }
+}
+
+template <typename T, typename TO>
+static hipError_t launch_tws(const IgemmArgs& a, hipStream_t s) {
+  constexpr int BKE = 64 / (int)sizeof(T);
+  if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
+  if (a.Cin % BKE || a.Cin / BKE > 8 || a.Ctot % 256 || a.n_ct != a.Ctot / 256 || a.src_br) return hipErrorInvalidValue;
+  const int n_mt = a.N * a.tiles_y * a.tiles_x;
+  int n_slots = kNumCUs / a.n_ct;   // one 512-thread block per CU (160 KiB of LDS)
+  if (n_slots < 1) n_slots = 1;
+  if (n_slots > n_mt) n_slots = n_mt;
+  hipLaunchKernelGGL((convT_ws_kernel<T, TO>), dim3(a.n_ct * n_slots), dim3(512), 0, s, a);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------
@@ -2461,6 +2618,7 @@ template <typename T, int TCW, int NS, int WRW, typename TO>
 static hipError_t launch_tring(const IgemmArgs& a, hipStream_t s) {
   constexpr int BR = 16 * TCW * WRW, LDS = NS * (BR * 64 + 256 * 64);
   if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
+  if (a.src_br && (WRW != 1 || a.src_br % BR || a.Ctot % a.src_br)) return hipErrorInvalidValue;
   if (a.Cin % (64 / (int)sizeof(T)) || a.Ctot % BR || a.n_ct != a.Ctot / BR) return hipErrorInvalidValue;
   const int n_mt = a.N * a.tiles_y * a.tiles_x;
   int n_slots = (kNumCUs * ((160 * 1024) / LDS)) / a.n_ct;
@@ -2567,7 +2725,10 @@ static hipError_t launch_up(int cfg, const IgemmArgs& a, hipStream_t s) {
       if constexpr (std::is_same<T, TO>::value) return launch_halo<T, 1, 4, 8, 2, EPI_UPSCATTER, 1>(a, s);
       break;
     case CFG_TRING_R128: return launch_tring<T, 8, 3, 1, TO>(a, s);
-    case CFG_TRING_R256: return launch_tring<T, 8, 4, 2, TO>(a, s);
+    case CFG_TRING_R256:   // Cin <= 256 (up2, an unfused up1): the weight-stationary variant, bitwise the same
+      if constexpr (sizeof(T) == 2)
+        if (a.convt_ws && a.Cin <= 8 * (64 / (int)sizeof(T)) && !a.src_br) return launch_tws<T, TO>(a, s);
+      return launch_tring<T, 8, 4, 2, TO>(a, s);
     default: break;
   }
   return hipErrorInvalidValue;
