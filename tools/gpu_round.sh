@@ -21,7 +21,7 @@ if [ "$MODE" != "skip-tests" ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
   echo smoke ok
 fi
-P="--no-cpu-baseline --no-latency --no-strong --no-fp32"
+P="--no-cpu-baseline --no-latency --no-strong --no-fp32 --no-cfg5"
 PASSES=("FETCH_SIZE" "WRITE_SIZE"
         "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE")
 profile() {   # profile SUFFIX TRAFFIC_JSON BENCH_ARGS...
