@@ -987,8 +987,8 @@ def test_small_batch_split_k_plan(dtype, monkeypatch):
 
 @pytest.mark.parametrize("dtype", ["mixed", "bf16"])
 def test_convtranspose_weight_stationary_matches_ring(dtype, monkeypatch):
-    """up2 (Cin = 256) on the weight-stationary ConvTranspose kernel (convT_ws_kernel, the default)
-    against the both-streamed ring (UNET_MI355X_CONVT_WS=0): the same tile, K order and fragments, so
+    """up2 (Cin = 256) on the weight-stationary ConvTranspose kernel (convT_ws_kernel, an A/B option:
+    UNET_MI355X_CONVT_WS=1) against the both-streamed ring (the default): the same tile, K order and fragments, so
     u2 and the logits agree bit for bit -- full pages (the walker wraps) and a ragged 48 x 80 shape
     (partial tiles), at a batch size outside the small-batch plan and inside it."""
     sd = syn.make_state_dict(3, 3, 3, profile="structured")

@@ -137,7 +137,10 @@ struct unet_handle {
   int ksplit_force[21] = {};
   unsigned xcd_rows = 0;   // bit i: 3x3 layer i walks with XCD-owned row tiles (UNET_MI355X_XCDROWS="i,...")
   int prio_hi = 0;         // UNET_MI355X_PRIO=1: waves 4-7 of the 8-wave kernels at s_setprio 1 (A/B option)
-  int convt_ws = 1;        // ConvTranspose with Cin <= 256 on the weight-stationary kernel (UNET_MI355X_CONVT_WS=0: off)
+  // ConvTranspose with Cin <= 256 on the weight-stationary kernel: bitwise the ring's, but +7 % on up2
+  // (its two-slot pixel ring gives one step of DMA cover; profiles/tune_r4f_convt_ws_rejected.txt), so an
+  // A/B option (UNET_MI355X_CONVT_WS=1), off
+  int convt_ws = 0;
   void* part = nullptr;   // the current forward's partial buffer (workspace region Buffers::part)
 };
 
