@@ -1007,3 +1007,26 @@ def test_convtranspose_weight_stationary_matches_ring(dtype, monkeypatch):
             m.close()
         assert torch.equal(st["1"][0], st["0"][0]), f"u2 differs at {n}x{h}x{w}"
         assert torch.equal(st["1"][1], st["0"][1]), f"logits differ at {n}x{h}x{w}"
+
+
+def test_small_batch_convtranspose_halves_bitwise(monkeypatch):
+    """The batch-1 plan's ConvTranspose on 128-row halves of the 256-row packing (up4, up3: the 4-wave
+    128-row ring reading the 8-wave ring's packing, csrc/unet_capi.cpp layer_split) is bitwise the
+    256-row ring: with the 3x3 layers forced unsplit (UNET_MI355X_KSPLIT_FORCE=i:1) the batch-1 forward
+    equals the one with the whole small-batch plan off (UNET_MI355X_KSPLIT=0), u4, u3 and logits."""
+    sd = syn.make_state_dict(0, 3, 3, profile="pretrained")
+    x = torch.from_numpy(syn.invoice_pages(1000, 1, 512, 512, 3)).to(DEV)
+    st = {}
+    for name, env in (("halves", {"UNET_MI355X_KSPLIT_FORCE": ",".join(f"{i}:1" for i in range(17))}),
+                      ("off", {"UNET_MI355X_KSPLIT": "0"})):
+        for k in ("UNET_MI355X_KSPLIT_FORCE", "UNET_MI355X_KSPLIT"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        m = make_model(sd, 3, "mixed")
+        with torch.no_grad():
+            lg = m(x)
+        torch.cuda.synchronize()
+        st[name] = {"u4": m.intermediate("u4").clone(), "u3": m.intermediate("u3").clone(), "logits": lg.clone()}
+        m.close()
+    assert _first_diff(st["halves"], st["off"]) == []
