@@ -137,6 +137,7 @@ struct unet_handle {
   int ksplit_force[21] = {};
   unsigned xcd_rows = 0;   // bit i: 3x3 layer i walks with XCD-owned row tiles (UNET_MI355X_XCDROWS="i,...")
   int prio_hi = 0;         // UNET_MI355X_PRIO=1: waves 4-7 of the 8-wave kernels at s_setprio 1 (A/B option)
+  unsigned prio_mask = 0;  // the same per launch: bit i = 3x3 layer i, 17 + j = ConvTranspose j (UNET_MI355X_PRIO_LAYERS)
   // ConvTranspose with Cin <= 256 on the weight-stationary kernel: bitwise the ring's, but +7 % on up2
   // (its two-slot pixel ring gives one step of DMA cover; profiles/tune_r4f_convt_ws_rejected.txt), so an
   // A/B option (UNET_MI355X_CONVT_WS=1), off
@@ -814,14 +815,18 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   if (const char* ks = std::getenv("UNET_MI355X_KSPLIT")) h->ksplit_max = std::atoi(ks);
   if (const char* pr = std::getenv("UNET_MI355X_PRIO")) h->prio_hi = std::atoi(pr) != 0;
   if (const char* cw = std::getenv("UNET_MI355X_CONVT_WS")) h->convt_ws = std::atoi(cw) != 0;
-  if (const char* xr = std::getenv("UNET_MI355X_XCDROWS")) {   // "i,j,..." 3x3 layer indices (A/B runs)
-    for (const char* p = xr; *p;) {
+  auto layer_mask = [](const char* v, int n) {   // "i,j,..." -> bit mask of indices < n
+    unsigned m = 0;
+    for (const char* p = v; p && *p;) {
       const int li = std::atoi(p);
-      if (li >= 0 && li < 17) h->xcd_rows |= 1u << li;
+      if (li >= 0 && li < n) m |= 1u << li;
       while (*p && *p != ',') ++p;
       if (*p == ',') ++p;
     }
-  }
+    return m;
+  };
+  h->xcd_rows = layer_mask(std::getenv("UNET_MI355X_XCDROWS"), 17);          // 3x3 layer indices (A/B runs)
+  h->prio_mask = layer_mask(std::getenv("UNET_MI355X_PRIO_LAYERS"), 21);     // + 17..20 = up4..up1
   if (const char* kf = std::getenv("UNET_MI355X_KSPLIT_FORCE")) {   // "i:ks,..." (A/B runs)
     std::string o(kf);
     size_t pos = 0;
@@ -1017,7 +1022,7 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.n_ct = L.ctot / cfg_rows(L.cfg);
   const int id = (&L >= h->L && &L < h->L + 17) ? (int)(&L - h->L) : 17 + (int)(&L - h->U);
   a.xcd_rows = id < 17 ? (int)((h->xcd_rows >> id) & 1u) : 0;
-  a.prio_hi = h->prio_hi;
+  a.prio_hi = h->prio_hi || ((h->prio_mask >> id) & 1u);
   a.convt_ws = h->convt_ws;
   const Split sp = layer_split(h, id, L, epi, N, H, W);
   int cfg = L.cfg;
