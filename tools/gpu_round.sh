@@ -6,8 +6,8 @@
 # the box) BEFORE the bench line runs, so the line's traffic comes from this commit.
 # Usage (from this container, after committing):
 #   gpurun --timeout 1200 -- "bash tools/gpu_round.sh TAG $(git rev-parse --short HEAD) [skip-tests]"
-# Copy gpurun_out/pmc_TAG/summary.json -> profiles/pmc_mixed_bs256.json (and _cfg5 ->
-# profiles/pmc_fp16_bs64_1024.json) afterwards.
+# Copy gpurun_out/pmc_TAG/summary.json -> profiles/pmc_mixed_bs256.json (_cfg5 ->
+# profiles/pmc_fp16_bs64_1024.json, _fp32 -> profiles/pmc_fp32_bs32.json) afterwards.
 set -e
 TAG=${1:-r3}
 COMMIT=${2:-unknown}
@@ -43,11 +43,15 @@ profile() {   # profile SUFFIX TRAFFIC_JSON BENCH_ARGS...
 SUMARGS=()
 profile "" pmc_mixed_bs256.json
 echo profiles ok
-timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
-echo bench ok
+# every traffic source of the bench line (headline, config 5, fp32 leg) from this commit before it runs
 SUMARGS=(--batch 64 --size 1024)
 profile _cfg5 pmc_fp16_bs64_1024.json --size 1024 --batch 64 --dtype fp16
 echo cfg5 profiles ok
+SUMARGS=(--batch 32 --esize 4)
+profile _fp32 pmc_fp32_bs32.json --batch 32 --dtype fp32
+echo fp32 profiles ok
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+echo bench ok
 timeout -k 10 300 python bench.py --size 1024 --batch 64 --dtype fp16 --steps 5 --warmup 3 --cpu-seconds 10 --no-latency \
     --no-strong > gpurun_out/bench_${TAG}_cfg5_fp16_1024.json 2> gpurun_out/bench_${TAG}_cfg5.err
 echo bench cfg5 ok
