@@ -649,14 +649,27 @@ __device__ __forceinline__ void mfma_taps(f32x4 (&acc)[TC][TP], const char* cons
 // double-buffered): the A fragments of all NT taps form ONE stream through a 3-register ring two
 // row groups ahead (crossing tap boundaries), and only the TP B fragments are double-buffered --
 // tap k+1's are read under the first TP row groups of tap k.
-template <typename T, int TC, int TP, int NT, typename Mid = NoMid>
+// ABL (ablation builds only, timing): 2 = the fragment reads without the MFMAs, 3 = the MFMAs on
+// register fragments without the LDS reads.
+template <typename T, int TC, int TP, int NT, int ABL = 0, typename Mid = NoMid>
 __device__ __forceinline__ void mfma_taps_astream(f32x4 (&acc)[TC][TP], const char* const (&hs)[NT],
                                                   const char* const (&ws)[NT], const int (&prow)[TP], Mid mid = Mid{}) {
   static_assert(TC >= TP && TC >= 3, "B prefetch spread over the row groups");
   frag_t ar[3], fb[2][TP];
-  auto lda = [&](int j) { return *reinterpret_cast<const frag_t*>(ws[j / TC] + (j % TC) * 16 * 64); };
+  frag_t rf = {};   // ABL 3: one real fragment per call (MFMAs on zeros would run at a higher clock)
+  if constexpr (ABL == 3) rf = *reinterpret_cast<const frag_t*>(hs[0] + prow[0]);
+  auto ldsread = [&](const char* p) {
+    if constexpr (ABL == 3) {
+      frag_t v = rf;
+      asm volatile("" : "+v"(v));
+      return v;
+    } else {
+      return *reinterpret_cast<const frag_t*>(p);
+    }
+  };
+  auto lda = [&](int j) { return ldsread(ws[j / TC] + (j % TC) * 16 * 64); };
 #pragma unroll
-  for (int p = 0; p < TP; ++p) fb[0][p] = *reinterpret_cast<const frag_t*>(hs[0] + prow[p]);
+  for (int p = 0; p < TP; ++p) fb[0][p] = ldsread(hs[0] + prow[p]);
   ar[0] = lda(0);
   ar[1] = lda(1);
   __builtin_amdgcn_sched_group_barrier(0x100, TP + 2, 0);
@@ -666,11 +679,13 @@ __device__ __forceinline__ void mfma_taps_astream(f32x4 (&acc)[TC][TP], const ch
     for (int t = 0; t < TC; ++t) {
       const int j = k * TC + t;
       if (j + 2 < NT * TC) ar[(j + 2) % 3] = lda(j + 2);
-      if (k + 1 < NT && t < TP) fb[(k + 1) & 1][t] = *reinterpret_cast<const frag_t*>(hs[k + 1] + prow[t]);
+      if (k + 1 < NT && t < TP) fb[(k + 1) & 1][t] = ldsread(hs[k + 1] + prow[t]);
       const frag_t af = ar[j % 3];
 #pragma unroll
-      for (int p = 0; p < TP; ++p)
-        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, fb[k & 1][p]));
+      for (int p = 0; p < TP; ++p) {
+        if constexpr (ABL == 2) asm volatile("" ::"v"(af), "v"(fb[k & 1][p]));
+        else mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, fb[k & 1][p]));
+      }
       if (j + 2 < NT * TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       if (k + 1 < NT && t < TP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
@@ -1473,6 +1488,14 @@ struct Ring8Geom {
   static constexpr int LDS_BYTES = XS_OFF + XS_BYTES;          // HS: exactly 160 KiB
 };
 
+// ablation builds only (ABL = 1, no barrier): the counted wait alone
+template <int N>
+__device__ __forceinline__ void wait_vm_only() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+  asm volatile("" ::: "memory");
+}
+
 // vmcnt(n) + barrier for a runtime (wave-uniform) n in [0, 15]
 __device__ __forceinline__ void wait_vm_barrier_rt(int n) {
   switch (n) {
@@ -1490,7 +1513,9 @@ __device__ __forceinline__ void wait_vm_barrier_rt(int n) {
 // HS = 1 (down1.3): down1.0 fused in, as in the 4-wave ring (its halo chunks are computed from a
 // 20 x 36 window of the pre-cast input on 16x16x16 MFMAs); needs WST (the loop then has a barrier
 // after every step: the window is re-filled while the halo of the next tile is computed from it).
-// ABL (timing-only ablation builds, `make abl`): 5 = no tile epilogue (the accumulators are kept
+// ABL (timing-only ablation builds, `make abl`; 3-tap 128-row ring): 1 = the counted waits without
+// the barriers, 2 = no MFMAs, 3 = no LDS fragment reads, 4 = no LDS-DMA in the loop (the slots keep
+// the prologue's bytes); 5 = no tile epilogue (the accumulators are kept
 // alive, nothing is stored) -- the per-tile epilogue's share of a layer, wrong outputs by construction;
 // 6 = the epilogue's arithmetic without its stores; 7 = its stores (zeros) without the arithmetic.
 template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0, int ABL = 0>
@@ -1568,6 +1593,20 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   // ring's last steps only (round 3).
   constexpr int WCC = PIECES % NW == 0 ? PIECES / NW : -1;
   auto loop_wait = [&](int young, bool hy) {
+    if constexpr (ABL == 1) {   // ablation: the counted wait without the barrier
+      if (young == NS - 2 && WCC >= 0) {
+        constexpr int base = (NS - 2) * (WCC < 0 ? 0 : WCC);
+        if (hy) wait_vm_only<base + HI>();
+        else wait_vm_only<base>();
+      } else {
+        wait_vm_only<0>();
+      }
+      return;
+    }
+    if constexpr (ABL == 4) {   // ablation: no DMA in the loop, so nothing to wait for
+      wait_vm_barrier<63>();
+      return;
+    }
     if constexpr (NS == 2 || WCC >= 0) {
       if (young == NS - 2) {
         constexpr int base = NS == 2 ? 0 : (NS - 2) * WCC;
@@ -1966,7 +2005,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     // instead of NS - 2; it is needed only at the chunk end)
     // this step's LDS-DMA (W(g+NS-1), then the next chunk's halo): issued from inside the tap
     // sequence, after its first MFMAs (mfma_taps* `mid`); the step paths without a hook issue it here
-    const bool dma_w = !WST && g + NS - 1 < total, dma_h = HS == 0 && hnext;
+    const bool dma_w = ABL != 4 && !WST && g + NS - 1 < total, dma_h = ABL != 4 && HS == 0 && hnext;
     auto dma = [&]() {
       if (dma_w) issue_w();
       if (dma_h) issue_halo();
@@ -2013,7 +2052,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         ws3[t] = wrow + wslot * SLOT + t * WSLOT;
       }
       if constexpr (TC * TP % (TC + TP) == 0) mfma_taps<T, TC, TP, 3>(acc, hs3, ws3, prow, dma);
-      else mfma_taps_astream<T, TC, TP, 3>(acc, hs3, ws3, prow, dma);
+      else mfma_taps_astream<T, TC, TP, 3, (ABL == 2 || ABL == 3) ? ABL : 0>(acc, hs3, ws3, prow, dma);
     } else {
 #pragma unroll
       for (int t = 0; t < TPS; ++t) step(g, hseq, tap * TPS + t, t);
@@ -2030,7 +2069,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       int young = total - 2 - g;
       young = young < 0 ? 0 : (young > NS - 2 ? NS - 2 : young);
       const bool hyoung = tap < NS - 1 && tap < SPC - 1 && hseq + 1 < hseq_end;
-      if (wskip > 0) { --wskip; wait_vm_barrier<63>(); }   // see ring_body
+      if (wskip > 0 && ABL != 1) { --wskip; wait_vm_barrier<63>(); }   // see ring_body
       else loop_wait(young, hyoung);
     }
     bool tile_end = false;
@@ -2672,7 +2711,7 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ, ABL>(a, s);
         break;
       case CFG_RING8_R128:
-        if constexpr (ABL >= 5 && ABL <= 7 && EPI != EPI_HEAD) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ, 0, ABL>(a, s);
+        if constexpr (ABL >= 1 && ABL <= 7 && EPI != EPI_HEAD) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ, 0, ABL>(a, s);
         break;
       case CFG_RING8_R64_T9:
         if constexpr (ABL >= 5 && ABL <= 7 && EPI != EPI_HEAD) return launch_ring8<T, 4, 2, EPI, 9, 0, TO, TQ, 0, ABL>(a, s);
