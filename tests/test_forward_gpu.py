@@ -1009,6 +1009,33 @@ def test_convtranspose_weight_stationary_matches_ring(dtype, monkeypatch):
         assert torch.equal(st["1"][1], st["0"][1]), f"logits differ at {n}x{h}x{w}"
 
 
+@pytest.mark.parametrize("dtype", ["mixed", "bf16"])
+def test_staggered_ring_matches_ring(dtype, monkeypatch):
+    """The staggered 3-tap 128-row ring (waves 4-7 one tap behind waves 0-3; UNET_MI355X_STAGGER, an A/B
+    option, csrc/unet_kernels.hip conv3x3_ring8_kernel ABL = kRing8Stagger) on every layer that runs the
+    8-wave 128-row ring (d2a .. c2a) against the default ring: the same MFMA order per accumulator, so the
+    logits agree bit for bit -- full pages (many tiles per walker) and a ragged 48 x 80 shape (walkers
+    with one tile: the lagging waves' first-step skip, tile-boundary epilogue and final tap)."""
+    sd = syn.make_state_dict(3, 3, 3, profile="structured")
+    layers = ",".join(str(i) for i in range(1, 14))
+    for n, h, w in ((6, 512, 512), (5, 48, 80)):
+        x = torch.from_numpy(syn.invoice_pages(7, n, h, w, 3)).to(DEV)
+        st = {}
+        for stg in (layers, ""):
+            monkeypatch.setenv("UNET_MI355X_STAGGER", stg)
+            m = make_model(sd, 3, dtype)
+            labels = m.native_handle(torch.device(DEV)).launch_labels()
+            for i in (2, 4, 11, 17):   # d2a, d3a, c4a, c2a
+                assert labels[i].endswith(", 0, 9>") == bool(stg), labels[i]
+            with torch.no_grad():
+                lg = m(x)
+            torch.cuda.synchronize()
+            st[stg] = (m.intermediate("c4").clone(), lg.clone())
+            m.close()
+        assert torch.equal(st[layers][0], st[""][0]), f"c4 differs at {n}x{h}x{w}"
+        assert torch.equal(st[layers][1], st[""][1]), f"logits differ at {n}x{h}x{w}"
+
+
 def test_small_batch_convtranspose_halves_bitwise(monkeypatch):
     """The batch-1 plan's ConvTranspose on 128-row halves of the 256-row packing (up4, up3: the 4-wave
     128-row ring reading the 8-wave ring's packing, csrc/unet_capi.cpp layer_split) is bitwise the

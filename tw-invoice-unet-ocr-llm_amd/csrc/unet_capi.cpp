@@ -94,6 +94,7 @@ struct Buffers {
 
 }  // namespace
 
+constexpr unsigned kPrioLayers = (1u << 0) | (1u << 1) | (1u << 16) | (1u << 17) | (1u << 18);
 struct unet_handle {
   unet_config cfg{};
   DType dt = DType::BF16;   // storage element type of the workspace (bf16 / f16 plans: 2 bytes)
@@ -137,7 +138,11 @@ struct unet_handle {
   int ksplit_force[21] = {};
   unsigned xcd_rows = 0;   // bit i: 3x3 layer i walks with XCD-owned row tiles (UNET_MI355X_XCDROWS="i,...")
   int prio_hi = 0;         // UNET_MI355X_PRIO=1: waves 4-7 of the 8-wave kernels at s_setprio 1 (A/B option)
-  unsigned prio_mask = 0;  // the same per launch: bit i = 3x3 layer i, 17 + j = ConvTranspose j (UNET_MI355X_PRIO_LAYERS)
+  unsigned stagger = 0;     // bit i: 3x3 layer i on the staggered ring (UNET_MI355X_STAGGER="i,..."; A/B option)
+  // the same per launch: bit i = 3x3 layer i, 17 + j = ConvTranspose j.  Default: down1.3, down2.0,
+  // conv1.3, up4, up3 -- the launches where it measured faster (profiles/tune_r4h_prio_layers.txt: the
+  // network −0.2 / −0.4 % in two in-process A/Bs, up3 −3 % in both); UNET_MI355X_PRIO_LAYERS overrides
+  unsigned prio_mask = kPrioLayers;
   // ConvTranspose with Cin <= 256 on the weight-stationary kernel: bitwise the ring's, but +7 % on up2
   // (its two-slot pixel ring gives one step of DMA cover; profiles/tune_r4f_convt_ws_rejected.txt), so an
   // A/B option (UNET_MI355X_CONVT_WS=1), off
@@ -610,6 +615,10 @@ std::string layer_label(const unet_handle* h, const Layer& L, int epi) {
   } else if (cfg_is_tring(cfg)) {
     std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, %d, %d, %s>", tname(L.dt), cfg == CFG_TRING_R256 ? 4 : 3,
                   cfg == CFG_TRING_R256 ? 2 : 1, tname(L.dto));
+  } else if (cfg == CFG_RING8_R128 && &L >= h->L && &L < h->L + 17 && ((h->stagger >> (&L - h->L)) & 1u) &&
+             epi != EPI_UPFUSE) {   // the staggered ring (launch_3x3)
+    std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, 8, 3, %d, 3, 0, %s, %s, 0, %d>", tname(L.dt), epi,
+                  tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto), kRing8Stagger);
   } else if (cfg_is_ring8(cfg)) {
     const int wst = cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;   // weight-stationary
     std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, %d, %d, %d, %d, %d, %s, %s, %d, 0>", tname(L.dt),
@@ -826,7 +835,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     return m;
   };
   h->xcd_rows = layer_mask(std::getenv("UNET_MI355X_XCDROWS"), 17);          // 3x3 layer indices (A/B runs)
-  h->prio_mask = layer_mask(std::getenv("UNET_MI355X_PRIO_LAYERS"), 21);     // + 17..20 = up4..up1
+  if (const char* pl = std::getenv("UNET_MI355X_PRIO_LAYERS")) h->prio_mask = layer_mask(pl, 21);   // + 17..20 = up4..up1
+  h->stagger = layer_mask(std::getenv("UNET_MI355X_STAGGER"), 17);
   if (const char* kf = std::getenv("UNET_MI355X_KSPLIT_FORCE")) {   // "i:ks,..." (A/B runs)
     std::string o(kf);
     size_t pos = 0;
@@ -1023,6 +1033,7 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   const int id = (&L >= h->L && &L < h->L + 17) ? (int)(&L - h->L) : 17 + (int)(&L - h->U);
   a.xcd_rows = id < 17 ? (int)((h->xcd_rows >> id) & 1u) : 0;
   a.prio_hi = h->prio_hi || ((h->prio_mask >> id) & 1u);
+  a.stagger = id < 17 ? (int)((h->stagger >> id) & 1u) : 0;
   a.convt_ws = h->convt_ws;
   const Split sp = layer_split(h, id, L, epi, N, H, W);
   int cfg = L.cfg;

@@ -71,6 +71,8 @@ struct IgemmArgs {
   // 8-wave kernels: waves 4-7 (the second-dispatched half, each SIMD's arbitration loser) run at
   // s_setprio 1 for the whole launch (MI355X_MICROARCH 'Two waves per SIMD' item 4; A/B option)
   int prio_hi;
+  // 3-tap 128-row 8-wave ring: waves 4-7 one tap behind waves 0-3 (the staggered ring, A/B option)
+  int stagger;
 };
 
 struct FirstConvArgs {
@@ -95,6 +97,7 @@ __host__ __device__ constexpr int first_tap_addr(int s) { return (int)((0x885522
 // fp32 path; the 64-byte-row ring family (persistent walkers, double-buffered halo, weight ring;
 // K order chunk32-major / tap-minor) is the 16-bit path; the ConvTranspose ring runs the 2x
 // upsamplers.  Selection per layer: unet_capi.cpp (defaults tuned on MI355X, profiles/tune_r1*).
+constexpr int kRing8Stagger = 9;   // conv3x3_ring8_kernel's variant slot (ABL) of the staggered ring
 enum Cfg : int {
   CFG_HALO_R64_W4 = 0,    // 64 rows x 16x16 pixels, 4 waves, 3 weight slots
   CFG_HALO_R64_W8 = 1,    // 64 rows, 8 waves
