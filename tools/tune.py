@@ -36,13 +36,14 @@ def main():
     x = torch.from_numpy(gen_pages(5, a.batch, a.size, 3)).to(dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     handles = []
+    base_env = dict(os.environ)
     for c in a.cands:
         lc, _, rest = c.partition("|")      # "<3x3 layer overrides>|<up overrides>|K=V;K=V (env)"
         uc, _, env = rest.partition("|")
+        os.environ.clear()                  # every candidate starts from the launch environment
+        os.environ.update(base_env)
         os.environ["UNET_MI355X_CFG"] = lc
         os.environ["UNET_MI355X_UPCFG"] = uc
-        for k in ("UNET_MI355X_PF",):
-            os.environ.pop(k, None)
         for kv in filter(None, env.split(";")):
             k, _, v = kv.partition("=")
             os.environ[k] = v

@@ -94,7 +94,6 @@ struct Buffers {
 
 }  // namespace
 
-constexpr unsigned kPrioLayers = (1u << 0) | (1u << 1) | (1u << 16) | (1u << 17) | (1u << 18);
 struct unet_handle {
   unet_config cfg{};
   DType dt = DType::BF16;   // storage element type of the workspace (bf16 / f16 plans: 2 bytes)
@@ -139,10 +138,11 @@ struct unet_handle {
   unsigned xcd_rows = 0;   // bit i: 3x3 layer i walks with XCD-owned row tiles (UNET_MI355X_XCDROWS="i,...")
   int prio_hi = 0;         // UNET_MI355X_PRIO=1: waves 4-7 of the 8-wave kernels at s_setprio 1 (A/B option)
   unsigned stagger = 0;     // bit i: 3x3 layer i on the staggered ring (UNET_MI355X_STAGGER="i,..."; A/B option)
-  // the same per launch: bit i = 3x3 layer i, 17 + j = ConvTranspose j.  Default: down1.3, down2.0,
-  // conv1.3, up4, up3 -- the launches where it measured faster (profiles/tune_r4h_prio_layers.txt: the
-  // network −0.2 / −0.4 % in two in-process A/Bs, up3 −3 % in both); UNET_MI355X_PRIO_LAYERS overrides
-  unsigned prio_mask = kPrioLayers;
+  // the same per launch (UNET_MI355X_PRIO_LAYERS="i,..."; bit i = 3x3 layer i, 17 + j = ConvTranspose j):
+  // on down1.3, down2.0, conv1.3, up4, up3 the network measured −0.2 / −0.4 % in two in-process A/Bs
+  // (profiles/tune_r4h_prio_layers.txt) and +0.3 % in two more (tune_r4i_stagger_rejected.txt, columns 2
+  // and 3): within the noise, so off
+  unsigned prio_mask = 0;
   // ConvTranspose with Cin <= 256 on the weight-stationary kernel: bitwise the ring's, but +7 % on up2
   // (its two-slot pixel ring gives one step of DMA cover; profiles/tune_r4f_convt_ws_rejected.txt), so an
   // A/B option (UNET_MI355X_CONVT_WS=1), off
