@@ -5,7 +5,8 @@
 # which is installed as the bench's roofline.traffic source (profiles/pmc_<dtype>_bs<B>[_<S>].json on
 # the box) BEFORE the bench line runs, so the line's traffic comes from this commit.
 # Usage (from this container, after committing):
-#   gpurun --timeout 1200 -- "bash tools/gpu_round.sh TAG $(git rev-parse --short HEAD) [skip-tests]"
+#   gpurun --timeout 1200 -- "bash tools/gpu_round.sh TAG $(git rev-parse --short HEAD) [skip-tests|no-bench|bench-only]"
+# (no-bench: tests, smoke and the profiles; bench-only: the two bench lines -- two calls within the time limit)
 # Copy gpurun_out/pmc_TAG/summary.json -> profiles/pmc_mixed_bs256.json (_cfg5 ->
 # profiles/pmc_fp16_bs64_1024.json, _fp32 -> profiles/pmc_fp32_bs32.json) afterwards.
 set -e
@@ -15,7 +16,7 @@ MODE=${3:-}
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-if [ "$MODE" != "skip-tests" ]; then
+if [ "$MODE" != "skip-tests" ] && [ "$MODE" != "bench-only" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 180 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
   echo tests ok
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
@@ -40,6 +41,7 @@ profile() {   # profile SUFFIX TRAFFIC_JSON BENCH_ARGS...
   python tools/prof_summary.py gpurun_out/prof_$TAG$S/run_kernel_trace.csv --min-grid 10000 > gpurun_out/prof_$TAG$S/summary.txt
   cp gpurun_out/pmc_$TAG$S/summary.json "profiles/$TJ"
 }
+if [ "$MODE" != "bench-only" ]; then
 SUMARGS=()
 profile "" pmc_mixed_bs256.json
 echo profiles ok
@@ -50,6 +52,8 @@ echo cfg5 profiles ok
 SUMARGS=(--batch 32 --esize 4)
 profile _fp32 pmc_fp32_bs32.json --batch 32 --dtype fp32
 echo fp32 profiles ok
+fi
+[ "$MODE" = "no-bench" ] && exit 0
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 echo bench ok
 timeout -k 10 300 python bench.py --size 1024 --batch 64 --dtype fp16 --steps 5 --warmup 3 --cpu-seconds 10 --no-latency \
