@@ -440,7 +440,7 @@ def cpu_baseline(args, sd, x, masks, C, S, extra=()):
     """The oracle (fp32 eager torch restating unet_model.py / inference.py) on this host's
     cores: batch-1 forward (images/s + the mask IoU of the GPU masks), batch-8 forward, and
     run_unet end to end (model load + resize + forward + masks + crops, inference.py:50-129).
-    extra: (name, x [1, C, h, w] CPU, bit-packed GPU masks [1, 3, h, w/8] CPU, GPU dtype) of other
+    extra: (name, x [n, C, h, w] CPU, bit-packed GPU masks [n, 3, h, w/8] CPU, GPU dtype) of other
     legs, whose masks are compared with the oracle's as `<name>_iou_vs_cpu`."""
     from PIL import Image
     from oracle import unet_oracle as orc
@@ -476,11 +476,13 @@ def cpu_baseline(args, sd, x, masks, C, S, extra=()):
         t_load = time.perf_counter() - t0
     more = {}
     for name, xe, me, dte in extra:
-        ref = orc.masks_from_logits(orc.unet_forward(sd_cpu, xe).numpy()[0])
-        got = np.unpackbits(me.numpy()[0], axis=-1, bitorder="little").astype(bool)
-        ie = [orc.mask_iou(got[i], ref[f]) for i, f in enumerate(orc.FIELDS)]
-        more[f"{name}_iou_vs_cpu"] = {"min": round(min(ie), 5), "mean": round(float(np.mean(ie)), 5), "images": 1,
-                                      "size": int(xe.shape[-1]), "gpu_dtype": dte}
+        ie = []
+        for j in range(xe.shape[0]):
+            ref = orc.masks_from_logits(orc.unet_forward(sd_cpu, xe[j:j + 1]).numpy()[0])
+            got = np.unpackbits(me.numpy()[j], axis=-1, bitorder="little").astype(bool)
+            ie += [orc.mask_iou(got[i], ref[f]) for i, f in enumerate(orc.FIELDS)]
+        more[f"{name}_iou_vs_cpu"] = {"min": round(min(ie), 5), "mean": round(float(np.mean(ie)), 5),
+                                      "images": int(xe.shape[0]), "size": int(xe.shape[-1]), "gpu_dtype": dte}
     return {**more, "value": round(done / t_bs1, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{done} of the bench images, batch 1, {S}x{S}, fp32 eager torch (oracle/unet_oracle.py), "
                       f"{threads} threads",
@@ -515,11 +517,15 @@ def fp32_leg(args, runner, dev):
     return out
 
 
+CFG5_IOU_PAGES = 3   # config-5 pages checked against the CPU oracle (~3 s each on 16 threads)
+
+
 def cfg5_leg(args, runner, dev):
     """BASELINE config 5 on one GPU: the reference's 5-level UNet(3,3) at 1024x1024, fp16 storage with
     fp32 accumulation, 64 images per GPU (config 5's per-rank share of batch 512 over 8 GPUs), fused
     bit-packed masks, timed like the headline (HIP events per launch for the roofline; traffic from
-    profiles/pmc_fp16_bs64_1024.json).  Returns (summary, first page, its masks) for the CPU check."""
+    profiles/pmc_fp16_bs64_1024.json).  Returns (summary, the first CFG5_IOU_PAGES pages, their masks) for
+    the CPU check."""
     B, S, C = args.cfg5_batch, 1024, args.channels
     model = runner.make_model("fp16")
     runner.reserve(B, S, model)
@@ -534,7 +540,7 @@ def cfg5_leg(args, runner, dev):
            "value": round(t["value"], 2), "unit": "images/s", "ms_per_step": round(t["ms_per_step"], 3),
            "steps": args.cfg5_steps, "whole_step_tflops": round(gflop / t["ms_per_step"], 1),
            "roofline": roof, "kernels": kernels, "layer_ms": layer_ms}
-    page, mk = x[:1].cpu(), masks[:1].cpu()
+    page, mk = x[:CFG5_IOU_PAGES].cpu(), masks[:CFG5_IOU_PAGES].cpu()   # distinct pages (unique=16)
     model.close()
     del x, masks
     return out, page, mk
