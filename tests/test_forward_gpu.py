@@ -1039,27 +1039,6 @@ def test_staggered_ring_matches_ring(dtype, monkeypatch):
         assert torch.equal(st[layers][1], st[""][1]), f"logits differ at {n}x{h}x{w}"
 
 
-def test_down13_window_prefetch_is_bitwise(monkeypatch):
-    """down1.3's L2 touch of the next-but-one input window (UNET_MI355X_XSPF=1: plain loads into a
-    register nobody reads, issued after the phase-1 wait) changes no byte of any output: c1, p1 and
-    the logits equal the run without it, on full pages (walkers with many tiles) and a ragged shape
-    (windows partly outside the image)."""
-    sd = syn.make_state_dict(3, 3, 3, profile="structured")
-    for n, h, w in ((6, 512, 512), (5, 48, 80)):
-        x = torch.from_numpy(syn.invoice_pages(9, n, h, w, 3)).to(DEV)
-        st = {}
-        for pf in ("1", "0"):
-            monkeypatch.setenv("UNET_MI355X_XSPF", pf)
-            m = make_model(sd, 3, "mixed")
-            with torch.no_grad():
-                lg = m(x)
-            torch.cuda.synchronize()
-            st[pf] = (m.intermediate("c1").clone(), m.intermediate("p1").clone(), lg.clone())
-            m.close()
-        for k, name in enumerate(("c1", "p1", "logits")):
-            assert torch.equal(st["1"][k], st["0"][k]), f"{name} differs at {n}x{h}x{w}"
-
-
 def test_small_batch_convtranspose_halves_bitwise(monkeypatch):
     """The batch-1 plan's ConvTranspose on 128-row halves of the 256-row packing (up4, up3: the 4-wave
     128-row ring reading the 8-wave ring's packing, csrc/unet_capi.cpp layer_split) is bitwise the

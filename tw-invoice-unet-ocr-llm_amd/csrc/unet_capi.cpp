@@ -138,7 +138,6 @@ struct unet_handle {
   unsigned xcd_rows = 0;   // bit i: 3x3 layer i walks with XCD-owned row tiles (UNET_MI355X_XCDROWS="i,...")
   int prio_hi = 0;         // UNET_MI355X_PRIO=1: waves 4-7 of the 8-wave kernels at s_setprio 1 (A/B option)
   unsigned stagger = 0;     // bit i: 3x3 layer i on the staggered ring (UNET_MI355X_STAGGER="i,..."; A/B option)
-  int xs_prefetch = 0;      // UNET_MI355X_XSPF=1: down1.3 touches the next-but-one input window into L2 (A/B)
   // the same per launch (UNET_MI355X_PRIO_LAYERS="i,..."; bit i = 3x3 layer i, 17 + j = ConvTranspose j):
   // on down1.3, down2.0, conv1.3, up4, up3 the network measured −0.2 / −0.4 % in two in-process A/Bs
   // (profiles/tune_r4h_prio_layers.txt) and +0.3 % in two more (tune_r4i_stagger_rejected.txt, columns 2
@@ -838,7 +837,6 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   h->xcd_rows = layer_mask(std::getenv("UNET_MI355X_XCDROWS"), 17);          // 3x3 layer indices (A/B runs)
   if (const char* pl = std::getenv("UNET_MI355X_PRIO_LAYERS")) h->prio_mask = layer_mask(pl, 21);   // + 17..20 = up4..up1
   h->stagger = layer_mask(std::getenv("UNET_MI355X_STAGGER"), 17);
-  if (const char* xp = std::getenv("UNET_MI355X_XSPF")) h->xs_prefetch = std::atoi(xp) != 0;
   if (const char* kf = std::getenv("UNET_MI355X_KSPLIT_FORCE")) {   // "i:ks,..." (A/B runs)
     std::string o(kf);
     size_t pos = 0;
@@ -1036,7 +1034,6 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.xcd_rows = id < 17 ? (int)((h->xcd_rows >> id) & 1u) : 0;
   a.prio_hi = h->prio_hi || ((h->prio_mask >> id) & 1u);
   a.stagger = id < 17 ? (int)((h->stagger >> id) & 1u) : 0;
-  a.xs_prefetch = h->xs_prefetch;
   a.convt_ws = h->convt_ws;
   const Split sp = layer_split(h, id, L, epi, N, H, W);
   int cfg = L.cfg;

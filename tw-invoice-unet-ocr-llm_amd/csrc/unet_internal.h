@@ -73,8 +73,6 @@ struct IgemmArgs {
   int prio_hi;
   // 3-tap 128-row 8-wave ring: waves 4-7 one tap behind waves 0-3 (the staggered ring, A/B option)
   int stagger;
-  // fused first conv (down1.3): touch the input window of the tile after next into L2 (A/B option)
-  int xs_prefetch;
 };
 
 struct FirstConvArgs {

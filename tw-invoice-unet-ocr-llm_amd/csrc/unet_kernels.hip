@@ -1979,23 +1979,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       compute_halo(i, tc, cbc, decltype(cbc)::value, C0{});
       compute_halo(i, tc, cbc, decltype(cbc)::value, C1{});
     };
-    // a.xs_prefetch: the window of tile i + 2 is touched into L2 in tile i's second phase (one
-    // 4-byte load per 64 bytes of it, into a register no one reads), so that the window DMA of tile
-    // i + 1's first phase -- one phase of cover, for a first touch of the input -- hits L2.  The load
-    // is issued after phase 1's vmcnt(0) and has landed by the next one; its register stays
-    // reserved until then (the empty asm that reads it after that wait).
-    uint32_t pf_sink = 0;
-    auto prefetch_xs = [&](const TileXY& tc) {
-      const int L = tid;
-      if (L < 20 * 5) {   // 20 window rows x 5 probes 64 B apart (the row's 288 bytes)
-        const int yy = L / 5, k = L - (L / 5) * 5;
-        const int iy = tc.ty * 16 + yy - 2, ix = tc.tx * TW - 2 + 8 * k;
-        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
-          const char* src = reinterpret_cast<const char*>(a.x0) + ((long long)(tc.n * H + iy) * W + ix) * 4 * sizeof(T);
-          asm volatile("global_load_dword %0, %1, off" : "=v"(pf_sink) : "v"(src) : "memory");
-        }
-      }
-    };
     TileXY cur = tile_xy(0);
     for (int item = 0; item < items; ++item) {
       const bool more = item + 1 < items;
@@ -2004,8 +1987,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       taps9(0);
       halo_all(item, cur, C1{});
       wait_vm_barrier<0>();
-      asm volatile("" ::"v"(pf_sink));   // the previous probe has landed (vmcnt(0) above)
-      if (a.xs_prefetch && item + 2 < items) prefetch_xs(tile_xy(item + 2));
       taps9(1);
       if (more) halo_all(item + 1, nxt, C0{});
       wait_vm_barrier<63>();   // barrier only: no load is waited for here
