@@ -49,6 +49,7 @@ def _cached_model(checkpoint_path: str, compute_dtype: str | None = None):
         m = _cache.get(key)
         if m is None:
             m = load_model(checkpoint_path, compute_dtype)
+            m._frozen = True   # private to the cache: its weights never change after the load
             _cache.clear()
             _cache[key] = m
         return m

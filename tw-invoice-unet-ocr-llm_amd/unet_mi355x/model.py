@@ -111,6 +111,10 @@ class UNet(nn.Module):
         self._lock = threading.Lock()
         self._sig_tensors = None
         self._sig_epoch = -1
+        # set by the drop-in's private model cache (inference._cached_model), whose model nobody can
+        # reach to modify: once packed, its handle skips the per-call weight signature (136 tensors,
+        # ~40-50 us of host time on the batch-1 call path)
+        self._frozen = False
 
     # ------------------------------------------------------------------ native plumbing
     def _apply(self, fn, *args, **kwargs):
@@ -135,6 +139,8 @@ class UNet(nn.Module):
         idx = device.index if device.index is not None else torch.cuda.current_device()
         with self._lock:
             h = self._handles.get(idx)
+            if h is not None and self._frozen and idx in self._packed_sig:
+                return h
             if h is None:
                 h = native.Handle(self.n_channels, self.n_classes, self.compute_dtype, idx,
                                   self.thresholds)
