@@ -132,7 +132,7 @@ def test_reference_512_logits(dtype):
     m.close()
 
 
-@pytest.mark.parametrize("c,n,h,w", [(3, 2, 64, 128), (1, 3, 96, 32), (3, 1, 160, 48)])
+@pytest.mark.parametrize("c,n,h,w", [(3, 2, 64, 128), (1, 3, 96, 32), (3, 1, 160, 48), (3, 2, 16, 16), (1, 1, 16, 80)])
 def test_fp32_vs_oracle_odd_shapes(c, n, h, w):
     sd = syn.make_state_dict(100 + h, c, 3, profile="structured")
     x = syn.uniform_batch(5 + w, n, c, h, w)
@@ -143,6 +143,24 @@ def test_fp32_vs_oracle_odd_shapes(c, n, h, w):
     err = rel_err(out, ref)
     print(f"fp32 {c}x{h}x{w} n={n}: rel err {err:.3e}")
     assert err <= TOL["fp32"]
+    m.close()
+
+
+@pytest.mark.parametrize("dtype", ["mixed", "bf16", "fp16"])
+@pytest.mark.parametrize("n,h,w", [(2, 16, 16), (1, 16, 112), (6, 16, 16)])
+def test_16bit_plans_at_the_minimum_size(dtype, n, h, w):
+    """The smallest input the reference accepts (H, W = 16: the bottleneck is 1 x 1 pixel, every tile
+    of every level is partial, the small-batch split-K plan at N <= 4 and the large-batch plan at N = 6)
+    against the fp32 oracle within the plan's tolerance."""
+    sd = syn.make_state_dict(200 + w, 3, 3, profile="structured")
+    x = syn.uniform_batch(7 + n, n, 3, h, w)
+    ref = orc.unet_forward(sd, torch.from_numpy(x)).numpy()
+    m = make_model(sd, 3, dtype)
+    with torch.no_grad():
+        out = m(torch.from_numpy(x).to(DEV)).cpu().numpy()
+    err = rel_err(out, ref)
+    print(f"{dtype} 3x{h}x{w} n={n}: rel err {err:.3e}")
+    assert err <= TOL[dtype]
     m.close()
 
 
