@@ -610,9 +610,7 @@ const char* tname(DType t) { return t == DType::F32 ? "float" : t == DType::BF16
 std::string layer_label(const unet_handle* h, const Layer& L, int epi) {
   char buf[160];
   const int cfg = L.cfg;
-  if (cfg == CFG_TRING_R256 && h->convt_ws == 2 && L.dt != DType::F32 && L.cin >= 128 && L.cin <= 256) {
-    std::snprintf(buf, sizeof buf, "convT_ws2_kernel<%s, %s>", tname(L.dt), tname(L.dto));   // launch_up: 4 .. 8 steps
-  } else if (cfg == CFG_TRING_R256 && h->convt_ws == 1 && L.dt != DType::F32 && L.cin <= 256) {   // Cin <= 8 steps
+  if (cfg == CFG_TRING_R256 && h->convt_ws && L.dt != DType::F32 && L.cin <= 256) {   // launch_up: Cin <= 8 steps
     std::snprintf(buf, sizeof buf, "convT_ws_kernel<%s, %s>", tname(L.dt), tname(L.dto));
   } else if (cfg_is_tring(cfg)) {
     std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, %d, %d, %s>", tname(L.dt), cfg == CFG_TRING_R256 ? 4 : 3,
@@ -825,7 +823,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   }
   if (const char* ks = std::getenv("UNET_MI355X_KSPLIT")) h->ksplit_max = std::atoi(ks);
   if (const char* pr = std::getenv("UNET_MI355X_PRIO")) h->prio_hi = std::atoi(pr) != 0;
-  if (const char* cw = std::getenv("UNET_MI355X_CONVT_WS")) h->convt_ws = std::atoi(cw);   // 1, 2: the variants
+  if (const char* cw = std::getenv("UNET_MI355X_CONVT_WS")) h->convt_ws = std::atoi(cw) != 0;
   auto layer_mask = [](const char* v, int n) {   // "i,j,..." -> bit mask of indices < n
     unsigned m = 0;
     for (const char* p = v; p && *p;) {
@@ -856,9 +854,7 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   DeviceGuard g(cfg->device);
   hipError_t e = hipEventCreateWithFlags(&h->done, hipEventDisableTiming);
   if (e != hipSuccess) { delete h; return fail(UNET_EHIP, std::string("hipEventCreate: ") + hipGetErrorString(e)); }
-  // zero page: conv padding source, + 64 B per K chunk (ring halo cursors; < 4 KB); at +8 KB a 16 KB
-  // scratch that convT_ws2_kernel's out-of-image lanes store into (kTrashOff), never read
-  std::vector<uint8_t> z(8192 + 16384, 0);
+  std::vector<uint8_t> z(4096, 0);   // zero page: conv padding source, + 64 B per K chunk (ring halo cursors)
   int rc = upload(h, &h->zero, z.data(), z.size());
   if (rc) { free_all(h); (void)hipEventDestroy(h->done); delete h; return rc; }
   *out = h;

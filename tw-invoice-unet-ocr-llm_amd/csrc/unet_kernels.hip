@@ -2645,177 +2645,6 @@ static hipError_t launch_tws(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ConvTranspose2d on 256-row x 128-pixel tiles with the row tile's weights resident (round 4, A/B:
-// UNET_MI355X_CONVT_WS=2), for 128 <= Cin <= 256 (up2).  The both-streamed ring runs at the per-CU
-// LDS-DMA piece rate (one 1 KiB piece per ~60 cycles); with the weights resident
-// and a 128-pixel tile, a step streams 8 KB of pixels and the tile's scatter stores are half as many,
-// so the pieces + stores per FLOP drop 1.5x, and four 8 KB pixel slots keep three steps in flight
-// (128 KB of weights + 32 KB = 160 KiB).  Tile = 8 x 16 input pixels; 8 waves = 4 row groups of 64 x 2
-// pixel groups of 64.  The counted waits include the tile-end stores: every lane stores (lanes of
-// pixels outside the image into a scratch area past the zero page), so each wave issues exactly
-// 2 TP store instructions per tile and no wait drains them.  Same K order per accumulator as the
-// ring, accumulators starting at the bias, so the outputs are bit for bit the ring's.
-constexpr int kTrashOff = 8192;   // scratch for the stores of out-of-image lanes: a.zero + kTrashOff
-template <typename T, typename TO>
-__global__ __launch_bounds__(512, 1) void convT_ws2_kernel(const IgemmArgs a) {
-  constexpr int NW = 8, TC = 4, TP = 4, BR = 256, BKE = 64 / (int)sizeof(T), SMAX = 8, NSB = 4;
-  constexpr int WI = BR / (16 * NW);   // A DMA pieces per wave and step (prologue only)
-  constexpr int ASTEP = BR * 64, BSLOT = 128 * 64, BOFF = SMAX * ASTEP;
-  constexpr int NST = 2 * TP;          // store instructions per wave and tile (store64_grouped: 2 each)
-  __shared__ __attribute__((aligned(16))) char lds[BOFF + NSB * BSLOT];
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const uint32_t lds0 = lds_addr_of(lds);
-  const int wr = wave >> 1, wp = wave & 1;   // 64-row group, 64-pixel group
-  int bid;
-  {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one walker
-    const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
-    const int b = blockIdx.x, x = b & 7, k = b >> 3;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-  }
-  const int ct = bid % a.n_ct;
-  const int slot = bid / a.n_ct;
-  const int n_slots = gridDim.x / a.n_ct;
-  const int H = a.H, W = a.W, tiles_y = (H + 7) >> 3, tiles_x = (W + 15) >> 4;
-  const int n_mt = a.N * tiles_y * tiles_x;
-  if (slot >= n_mt) return;
-  const int items = (n_mt - slot + n_slots - 1) / n_slots;
-  const int S = a.Cin / BKE;                  // 4 .. 8 (launcher)
-  const int total = items * S;
-  const char* in = reinterpret_cast<const char*>(a.in);
-  const char* zero = reinterpret_cast<const char*>(a.zero);
-  auto tile_of = [&](int i, int& n, int& ty, int& tx) {
-    int mt = slot + i * n_slots;
-    tx = mt % tiles_x;
-    mt /= tiles_x;
-    ty = mt % tiles_y;
-    n = mt / tiles_y;
-  };
-  {  // the row tile's weights, all S steps (the ring's packing, [ct][s][256 rows][64 B])
-    const char* wct = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * ASTEP + wave * WI * 1024;
-    const uint32_t wlane = (lane >> 2) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
-    for (int st = 0; st < S; ++st)
-#pragma unroll
-      for (int j = 0; j < WI; ++j)
-        glds16_sv(wct + (size_t)st * ASTEP + j * 1024, wlane, lds0 + st * ASTEP + (wave * WI + j) * 1024);
-  }
-  // pixel stream: one piece per wave and step (16 pixel rows); per-lane pointer set at a tile's first step
-  int iss_c = 0, iss_i = 0, iss_slot = 0;
-  const char* bsrc = zero;
-  auto issue_b = [&]() {
-    if (iss_c == 0) {
-      int n, ty, tx;
-      tile_of(iss_i, n, ty, tx);
-      const int r = wave * 16 + (lane >> 2), py = r >> 4, px = r & 15;
-      const int iy = ty * 8 + py, ix = tx * 16 + px;
-      const int chk = ((lane & 3) ^ ((py & 1) << 1)) << 4;
-      bsrc = iy < H && ix < W ? in + ((long long)(n * H + iy) * W + ix) * a.ldi * (long long)sizeof(T) + chk : zero + chk;
-    }
-    glds16_s(bsrc + iss_c * BKE * (int)sizeof(T), lds0 + BOFF + iss_slot * BSLOT + wave * 1024);
-    iss_slot = (iss_slot + 1) & (NSB - 1);
-    if (++iss_c == S) { iss_c = 0; ++iss_i; }
-  };
-  const int pre = total < NSB - 1 ? total : NSB - 1;
-  for (int k = 0; k < pre; ++k) issue_b();
-  const int col = lane & 15, q = lane >> 4;
-  f32x4 bv[TC];
-#pragma unroll
-  for (int t = 0; t < TC; ++t) bv[t] = *reinterpret_cast<const f32x4*>(a.bias + ct * BR + wr * 64 + 16 * q + 4 * t);
-  f32x4 acc[TC][TP];
-  auto init_acc = [&]() {
-#pragma unroll
-    for (int t = 0; t < TC; ++t)
-#pragma unroll
-      for (int p = 0; p < TP; ++p) acc[t][p] = bv[t];
-  };
-  init_acc();
-  int prow[TP];
-#pragma unroll
-  for (int p = 0; p < TP; ++p) {
-    int py, px;
-    pix_of((wp * TP + p) * 16 + col, py, px);
-    prow[p] = (py * 16 + px) * 64 + ((q ^ ((py & 1) << 1)) << 4);
-  }
-  const int wrow = (wr * 64 + col) * 64 + ((q ^ ((col >> 1) & 3)) << 4);
-  TO* const trash = reinterpret_cast<TO*>(const_cast<char*>(zero) + kTrashOff) + lane * 64;
-  // the tile's scatter: every lane stores (out-of-image lanes into the scratch), NST instructions
-  auto epilogue = [&](int it) {
-    int n, ty, tx;
-    tile_of(it, n, ty, tx);
-    const int row0 = ct * BR + wr * 64, cout = a.Cout;
-    const int ab = row0 / cout, o0 = row0 - ab * cout;   // a 64-row group lies in one (a, b) quadrant
-#pragma unroll
-    for (int p = 0; p < TP; ++p) {
-      int py, px;
-      pix_of((wp * TP + p) * 16 + col, py, px);
-      const int oy = ty * 8 + py, ox = tx * 16 + px;
-      const bool inside = oy < H && ox < W;
-      float v[16];
-#pragma unroll
-      for (int t = 0; t < TC; ++t)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[t * 4 + e] = acc[t][p][e];
-      const int Y = 2 * oy + (ab >> 1), X = 2 * ox + (ab & 1);
-      TO* grp = inside ? reinterpret_cast<TO*>(a.out) + ((long long)(n * 2 * H + Y) * (2 * W) + X) * a.ldo + a.out_off + o0
-                       : trash;
-      store64_grouped<TO>(grp, v);
-    }
-    init_acc();
-  };
-  // A (all steps) and step 0's pixels landed; steps 1, 2 may stay in flight
-  wait_vm_barrier_rt(pre - 1);
-
-  int c = 0, item = 0, st_age = 2;   // steps since the last tile's stores (2+: none among the young ops)
-  for (int g = 0; g < total; ++g) {
-    const bool dma = g + NSB - 1 < total;
-    const char* As = lds + c * ASTEP + wrow;
-    const char* Bs = lds + BOFF + (g & (NSB - 1)) * BSLOT;
-    frag_t bq[TP], ar[3];
-#pragma unroll
-    for (int p = 0; p < TP; ++p) bq[p] = *reinterpret_cast<const frag_t*>(Bs + prow[p]);
-    ar[0] = *reinterpret_cast<const frag_t*>(As);
-    ar[1] = *reinterpret_cast<const frag_t*>(As + 16 * 64);
-    __builtin_amdgcn_sched_group_barrier(0x100, TP + 2, 0);
-#pragma unroll
-    for (int t = 0; t < TC; ++t) {
-      if (t + 2 < TC) ar[(t + 2) % 3] = *reinterpret_cast<const frag_t*>(As + (t + 2) * 16 * 64);
-      const frag_t af = ar[t % 3];
-#pragma unroll
-      for (int p = 0; p < TP; ++p)
-        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
-      if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
-      // step g+3's pixels into the slot step g-1 used (every wave's reads of it are behind the last barrier)
-      if (t == 1 && dma) issue_b();
-    }
-    // step g+1's pixels landed.  Younger vector-memory operations, in issue order: step g+2's piece,
-    // the stores of a tile that ended one or two steps ago (S >= 4: at most one such tile), step g+3's
-    // piece -- they stay in flight
-    const int young = (g + 2 < total ? 1 : 0) + (dma ? 1 : 0) + (st_age < 2 ? NST : 0);
-    wait_vm_barrier_rt(young);
-    ++st_age;
-    if (++c == S) {
-      c = 0;
-      epilogue(item);
-      ++item;
-      st_age = 0;
-    }
-  }
-}
-
-template <typename T, typename TO>
-static hipError_t launch_tws2(const IgemmArgs& a, hipStream_t s) {
-  constexpr int BKE = 64 / (int)sizeof(T);
-  if (a.Cin % BKE || a.Cin / BKE < 4 || a.Cin / BKE > 8 || a.Ctot % 256 || a.n_ct != a.Ctot / 256 || a.src_br ||
-      a.Cout % 64)
-    return hipErrorInvalidValue;
-  const int n_mt = a.N * ((a.H + 7) / 8) * ((a.W + 15) / 16);
-  int n_slots = kNumCUs / a.n_ct;   // one 512-thread block per CU (160 KiB of LDS)
-  if (n_slots < 1) n_slots = 1;
-  if (n_slots > n_mt) n_slots = n_mt;
-  hipLaunchKernelGGL((convT_ws2_kernel<T, TO>), dim3(a.n_ct * n_slots), dim3(512), 0, s, a);
-  return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------------
 // first conv: C in {1,3} input channels, fp32 NCHW in, 64 channels NHWC out.
 // K = 9*C is far too short for MFMA; it is a VALU direct conv, bound by HBM
@@ -3087,12 +2916,9 @@ static hipError_t launch_up(int cfg, const IgemmArgs& a, hipStream_t s) {
       if constexpr (std::is_same<T, TO>::value) return launch_halo<T, 1, 4, 8, 2, EPI_UPSCATTER, 1>(a, s);
       break;
     case CFG_TRING_R128: return launch_tring<T, 8, 3, 1, TO>(a, s);
-    case CFG_TRING_R256:   // Cin <= 256 (up2, an unfused up1): the weight-stationary variants, bitwise the same
-      if constexpr (sizeof(T) == 2) {
-        constexpr int BKE = 64 / (int)sizeof(T);
-        if (a.convt_ws == 2 && a.Cin >= 4 * BKE && a.Cin <= 8 * BKE && !a.src_br) return launch_tws2<T, TO>(a, s);
-        if (a.convt_ws == 1 && a.Cin <= 8 * BKE && !a.src_br) return launch_tws<T, TO>(a, s);
-      }
+    case CFG_TRING_R256:   // Cin <= 256 (up2, an unfused up1): the weight-stationary variant, bitwise the same
+      if constexpr (sizeof(T) == 2)
+        if (a.convt_ws && a.Cin <= 8 * (64 / (int)sizeof(T)) && !a.src_br) return launch_tws<T, TO>(a, s);
       return launch_tring<T, 8, 4, 2, TO>(a, s);
     default: break;
   }
