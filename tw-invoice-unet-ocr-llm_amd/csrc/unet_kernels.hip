@@ -2658,13 +2658,13 @@ __global__ __launch_bounds__(256) void first_conv_kernel(const FirstConvArgs a) 
   for (int i = threadIdx.x; i < 64 * KW; i += 256) ws[i] = a.w[i];
   if (threadIdx.x < 64) bs[threadIdx.x] = a.b[threadIdx.x];
   __syncthreads();
-  const long long total = (long long)a.N * a.H * a.W;
-  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int total = a.N * a.H * a.W;   // <= 2^30 (unet_capi's shape check): 32-bit index math
+  const int pix = blockIdx.x * 256 + threadIdx.x;
   if (pix >= total) return;
-  const int x = (int)(pix % a.W);
-  const long long t = pix / a.W;
-  const int y = (int)(t % a.H);
-  const int n = (int)(t / a.H);
+  const int x = pix % a.W;
+  const int t = pix / a.W;
+  const int y = t % a.H;
+  const int n = t / a.H;
   float xin[KW];
 #pragma unroll
   for (int c = 0; c < C; ++c)
@@ -2676,7 +2676,7 @@ __global__ __launch_bounds__(256) void first_conv_kernel(const FirstConvArgs a) 
         const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
         xin[(c * 3 + ky) * 3 + kx] = ok ? a.x[(((long long)n * C + c) * a.H + iy) * a.W + ix] : 0.f;
       }
-  T* dst = reinterpret_cast<T*>(a.out) + pix * 64;
+  T* dst = reinterpret_cast<T*>(a.out) + (long long)pix * 64;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     float v[16];
@@ -3048,13 +3048,25 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const IgemmArgs a) {
   const int H = a.H, W = a.W;
   const int Hs = EPI == EPI_POOL ? H / 2 : H, Ws = EPI == EPI_POOL ? W / 2 : W;
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)a.N * Hs * Ws * R8) return;
-  const int r0 = 8 * (int)(idx % R8);
-  long long pix = idx / R8;
-  const int x = (int)(pix % Ws);
-  pix /= Ws;
-  const int y = (int)(pix % Hs);
-  const int n = (int)(pix / Hs);
+  const long long n_idx = (long long)a.N * Hs * Ws * R8;
+  if (idx >= n_idx) return;
+  int r0, x, y, n;
+  if (n_idx < (1LL << 31)) {   // 32-bit index math (64-bit divisions cost microseconds per launch here)
+    const int id = (int)idx;
+    r0 = 8 * (id % R8);
+    int p = id / R8;
+    x = p % Ws;
+    p /= Ws;
+    y = p % Hs;
+    n = p / Hs;
+  } else {
+    r0 = 8 * (int)(idx % R8);
+    long long pix = idx / R8;
+    x = (int)(pix % Ws);
+    pix /= Ws;
+    y = (int)(pix % Hs);
+    n = (int)(pix / Hs);
+  }
   const long long slice = (long long)a.N * H * W * a.Ctot;
   const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + r0), b1 = *reinterpret_cast<const f32x4*>(a.bias + r0 + 4);
   auto reduce = [&](int yy, int xx, float (&v)[8]) {
@@ -3249,12 +3261,14 @@ __global__ __launch_bounds__(256) void x_to_px4_kernel(const void* __restrict__ 
     // the common case (fp32 NCHW: bench.py, run_unet's preprocess output): four pixels per thread,
     // one 16-byte load per channel plane and two 16-byte stores (4-byte loads and 8-byte stores ran
     // at 3.9 TB/s); the same casts, so bitwise equal to the generic loop below
+    // 32-bit index math: N*H*W <= 2^30 (unet_capi's shape check); the 64-bit division it replaces
+    // made this kernel 30 us at batch 1 against 6 us (tools/calib/precast_bs1.hip)
     const float* xf = static_cast<const float*>(x);
-    const long long quads = P / 4;
-    for (long long qd = (long long)blockIdx.x * 256 + threadIdx.x; qd < quads; qd += (long long)gridDim.x * 256) {
-      const long long i = 4 * qd, n = i / HW, hw = i - n * HW;   // HW % 4 == 0: one image per quad
+    const int quads = (int)(P / 4), hw32 = (int)HW;
+    for (int qd = blockIdx.x * 256 + threadIdx.x; qd < quads; qd += gridDim.x * 256) {
+      const int i = 4 * qd, n = i / hw32, hw = i - n * hw32;   // HW % 4 == 0: one image per quad
       float4 v[3] = {};
-      for (int c = 0; c < C; ++c) v[c] = *reinterpret_cast<const float4*>(xf + (n * C + c) * HW + hw);
+      for (int c = 0; c < C; ++c) v[c] = *reinterpret_cast<const float4*>(xf + ((long long)n * C + c) * HW + hw);
       t8 o0, o1;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -3270,8 +3284,9 @@ __global__ __launch_bounds__(256) void x_to_px4_kernel(const void* __restrict__ 
     }
     return;
   }
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < P; i += (long long)gridDim.x * 256) {
-    const long long n = i / HW, hw = i - n * HW;
+  const int P32 = (int)P, hw32 = (int)HW;   // <= 2^30 (see above)
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < P32; i += gridDim.x * 256) {
+    const int n = i / hw32, hw = i - n * hw32;
     t4 v;
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] = (T)(c < C ? input_at(x, layout, xdt, n, c, hw, C, HW) : 0.f);
@@ -3303,9 +3318,10 @@ hipError_t launch_x_to_px4(DType t, const void* x, int layout, int xdt, int N, i
 __global__ __launch_bounds__(256) void x_to_nchw_f32_kernel(const void* __restrict__ x, int layout, int xdt, int N,
                                                            int C, int H, int W, float* __restrict__ out) {
   const long long HW = (long long)H * W, total = (long long)N * C * HW;
+  const int hw32 = (int)HW;   // the pixel index stays 32-bit; (n, c) from the plane index
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const long long hw = i % HW, nc = i / HW;
-    out[i] = input_at(x, layout, xdt, nc / C, (int)(nc % C), hw, C, HW);
+    const int nc = (int)(i / hw32), hw = (int)(i - (long long)nc * hw32);
+    out[i] = input_at(x, layout, xdt, nc / C, nc % C, hw, C, HW);
   }
 }
 
