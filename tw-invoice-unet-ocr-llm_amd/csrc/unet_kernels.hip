@@ -3261,14 +3261,20 @@ __global__ __launch_bounds__(256) void x_to_px4_kernel(const void* __restrict__ 
     // the common case (fp32 NCHW: bench.py, run_unet's preprocess output): four pixels per thread,
     // one 16-byte load per channel plane and two 16-byte stores (4-byte loads and 8-byte stores ran
     // at 3.9 TB/s); the same casts, so bitwise equal to the generic loop below
-    // 32-bit index math: N*H*W <= 2^30 (unet_capi's shape check); the 64-bit division it replaces
-    // made this kernel 30 us at batch 1 against 6 us (tools/calib/precast_bs1.hip)
+    // 32-bit index math: N*H*W <= 2^30 (unet_capi's shape check); with the named loads below, the
+    // batch-1 launch 30 -> ~6 us in isolation (tools/calib/precast_bs1.hip)
     const float* xf = static_cast<const float*>(x);
     const int quads = (int)(P / 4), hw32 = (int)HW;
     for (int qd = blockIdx.x * 256 + threadIdx.x; qd < quads; qd += gridDim.x * 256) {
       const int i = 4 * qd, n = i / hw32, hw = i - n * hw32;   // HW % 4 == 0: one image per quad
-      float4 v[3] = {};
-      for (int c = 0; c < C; ++c) v[c] = *reinterpret_cast<const float4*>(xf + ((long long)n * C + c) * HW + hw);
+      // the planes as three named loads (a runtime-C loop into a float4[3] was promoted to LDS and,
+      // with the 64-bit division, held the batch-1 launch at 30 us)
+      const float* px0 = xf + (long long)n * C * HW + hw;
+      const float4 z4 = {0.f, 0.f, 0.f, 0.f};
+      float4 v[3];
+      v[0] = *reinterpret_cast<const float4*>(px0);
+      v[1] = C > 1 ? *reinterpret_cast<const float4*>(px0 + HW) : z4;
+      v[2] = C > 2 ? *reinterpret_cast<const float4*>(px0 + 2 * HW) : z4;
       t8 o0, o1;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
