@@ -3265,9 +3265,23 @@ __global__ __launch_bounds__(256) void x_to_px4_kernel(const void* __restrict__ 
     // batch-1 launch 30 -> ~6 us in isolation (tools/calib/precast_bs1.hip)
     const float* xf = static_cast<const float*>(x);
     const int quads = (int)(P / 4), hw32 = (int)HW;
+    if (C == 3) {   // the network's input (RGB): three unconditional plane loads per quad
+      for (int qd = blockIdx.x * 256 + threadIdx.x; qd < quads; qd += gridDim.x * 256) {
+        const int i = 4 * qd, n = i / hw32, hw = i - n * hw32;   // HW % 4 == 0: one image per quad
+        const float* px0 = xf + (long long)n * 3 * HW + hw;
+        const float4 v0 = *reinterpret_cast<const float4*>(px0);
+        const float4 v1 = *reinterpret_cast<const float4*>(px0 + HW);
+        const float4 v2 = *reinterpret_cast<const float4*>(px0 + 2 * HW);
+        t8 o0 = {(T)v0.x, (T)v1.x, (T)v2.x, (T)0.f, (T)v0.y, (T)v1.y, (T)v2.y, (T)0.f};
+        t8 o1 = {(T)v0.z, (T)v1.z, (T)v2.z, (T)0.f, (T)v0.w, (T)v1.w, (T)v2.w, (T)0.f};
+        reinterpret_cast<t8*>(out)[2 * qd] = o0;
+        reinterpret_cast<t8*>(out)[2 * qd + 1] = o1;
+      }
+      return;
+    }
     for (int qd = blockIdx.x * 256 + threadIdx.x; qd < quads; qd += gridDim.x * 256) {
       const int i = 4 * qd, n = i / hw32, hw = i - n * hw32;   // HW % 4 == 0: one image per quad
-      // the planes as three named loads (a runtime-C loop into a float4[3] was promoted to LDS and,
+      // the planes as named loads (a runtime-C loop into a float4[3] was promoted to LDS and,
       // with the 64-bit division, held the batch-1 launch at 30 us)
       const float* px0 = xf + (long long)n * C * HW + hw;
       const float4 z4 = {0.f, 0.f, 0.f, 0.f};
