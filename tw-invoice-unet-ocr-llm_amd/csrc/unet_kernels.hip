@@ -2653,11 +2653,11 @@ static hipError_t launch_tws(const IgemmArgs& a, hipStream_t s) {
 template <typename T, int C>
 __global__ __launch_bounds__(256) void first_conv_kernel(const FirstConvArgs a) {
   constexpr int KW = 9 * C;
-  // The weights and biases are read straight from global memory at wave-uniform, compile-time offsets,
-  // so they arrive by scalar loads into SGPRs and feed the FMAs as scalar operands.  Staged in LDS,
-  // every FMA cost a broadcast ds_read: the kernel was LDS-read-bound (0.8 ms at bs32, 40 us at bs1).
-  const float* __restrict__ ws = a.w;
-  const float* __restrict__ bs = a.b;
+  __shared__ float ws[64 * KW];
+  __shared__ float bs[64];
+  for (int i = threadIdx.x; i < 64 * KW; i += 256) ws[i] = a.w[i];
+  if (threadIdx.x < 64) bs[threadIdx.x] = a.b[threadIdx.x];
+  __syncthreads();
   const int total = a.N * a.H * a.W;   // <= 2^30 (unet_capi's shape check): 32-bit index math
   const int pix = blockIdx.x * 256 + threadIdx.x;
   if (pix >= total) return;
