@@ -110,3 +110,19 @@ def test_crops_from_boxes_and_stats_equal_reference_crops():
                 if a[k] is not None:
                     assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]))
                     assert np.array_equal(np.asarray(a[k]), np.asarray(c[k]))
+
+
+def test_photo_array_equals_numpy_view_of_the_photo():
+    """run_unet's one-pass photo packing (inference.photo_array) == np.asarray(photo), the bytes the
+    reference's preprocess reads (inference.py:30-44): RGB and L, odd sizes, a 1x1 and a 12 MP photo;
+    other modes go through np.asarray unchanged."""
+    from PIL import Image
+    from unet_mi355x.inference import photo_array
+    rng = np.random.default_rng(11)
+    for shape, mode in [((400, 600, 3), "RGB"), ((401, 599, 3), "RGB"), ((37, 23), "L"), ((1, 1, 3), "RGB"),
+                        ((3024, 4032, 3), "RGB")]:
+        pil = Image.fromarray(rng.integers(0, 256, shape, dtype=np.uint8), mode)
+        got = photo_array(pil)
+        assert got.dtype == np.uint8 and got.shape == shape and np.array_equal(got, np.asarray(pil)), shape
+    rgba = Image.fromarray(rng.integers(0, 256, (5, 7, 4), dtype=np.uint8), "RGBA")
+    assert np.array_equal(photo_array(rgba), np.asarray(rgba))

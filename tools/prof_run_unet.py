@@ -1,0 +1,116 @@
+"""Where the batch-1 run_unet time goes beyond the forward (GPU box).
+
+Times the drop-in run_unet (inference.py:50-129 restated in unet_mi355x/inference.py) on a
+600x400 RGB photo at the fp32 default and the mixed plan: the end-to-end median, a cProfile of
+the host side, and each stage of the call on its own (host wall time with a synchronisation
+after the stage, and the device time of the stage between HIP events).
+Usage: python tools/prof_run_unet.py [--calls 50]
+"""
+import argparse
+import cProfile
+import io
+import os
+import pstats
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tw-invoice-unet-ocr-llm_amd"))
+from PIL import Image  # noqa: E402
+from unet_mi355x import inference as inf, native  # noqa: E402
+from unet_mi355x.model import UNet  # noqa: E402
+
+
+def med(f, n):
+    lat = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        f()
+        lat.append(time.perf_counter() - t0)
+    return 1e3 * float(np.median(lat))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--calls", type=int, default=50)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    inf.DEVICE = "cuda:0"
+    torch.manual_seed(0)
+    sd = UNet(3, 3).state_dict()
+    rng = np.random.default_rng(7)
+    photo = (rng.random((400, 600, 3)) * 60 + 150).astype(np.uint8)
+    photo[100:140, 200:420] = 20
+    pil = Image.fromarray(photo, "RGB")
+    with tempfile.TemporaryDirectory() as td:
+        ck = os.path.join(td, "best_unet_model.pth")
+        torch.save(sd, ck)
+        for dtype in ("fp32", "mixed"):
+            for _ in range(5):
+                inf.run_unet(pil, ck, compute_dtype=dtype)
+            torch.cuda.synchronize()
+            total = med(lambda: inf.run_unet(pil, ck, compute_dtype=dtype), args.calls)
+            print(f"[{dtype}] run_unet median {total:.3f} ms over {args.calls} calls", flush=True)
+            pr = cProfile.Profile()
+            pr.enable()
+            for _ in range(args.calls):
+                inf.run_unet(pil, ck, compute_dtype=dtype)
+            pr.disable()
+            s = io.StringIO()
+            pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(22)
+            print(s.getvalue(), flush=True)
+
+            # the stages of run_unet, each followed by a synchronisation
+            model = inf._cached_model(ck, dtype)
+            st = inf._staging[str(inf.DEVICE)]
+            stream = torch.cuda.current_stream(dev)
+            arr = np.asarray(pil)
+            img = st.upload(arr)
+            stages = {
+                "cached_model": lambda: inf._cached_model(ck, dtype),
+                "asarray": lambda: np.asarray(pil),
+                "upload": lambda: st.upload(arr),
+                "preprocess": lambda: model.preprocess(img, inf.IMG_SIZE, out=st.x[0]),
+                "forward_boxes": lambda: model.forward_boxes(st.x, masks="u8", out=(st.m, st.b)),
+                "crop_stats": lambda: native.crop_stats(img, st.b[0], inf.IMG_SIZE, inf.IMG_SIZE, inf.CROP_PAD,
+                                                        st.r, st.s, stream.cuda_stream),
+                "d2h_4": lambda: (st.hr.copy_(st.r, non_blocking=True), st.hs.copy_(st.s, non_blocking=True),
+                                  st.hm.copy_(st.m, non_blocking=True), st.hb.copy_(st.b, non_blocking=True)),
+                "d2h_masks_only": lambda: st.hm.copy_(st.m, non_blocking=True),
+                "mask_bool_copy": lambda: st.hm.numpy()[0].view(np.bool_).copy(),
+                "crops": lambda: {k: inf.crop_from_stats(pil, st.hr.numpy()[i], st.hs.numpy()[i], 3)
+                                  for i, k in enumerate(inf.FIELDS)},
+                "sync_only": lambda: None,
+            }
+            for name, f in stages.items():
+                def g():
+                    f()
+                    stream.synchronize()
+                for _ in range(3):
+                    g()
+                host = med(g, args.calls)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(20):
+                    f()
+                e1.record()
+                torch.cuda.synchronize()
+                print(f"[{dtype}] {name:16s} host+sync {host:.4f} ms   device {e0.elapsed_time(e1) / 20:.4f} ms",
+                      flush=True)
+            with torch.no_grad():
+                x = st.x
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(20):
+                    model.forward_boxes(x, masks="u8", out=(st.m, st.b))
+                e1.record()
+                torch.cuda.synchronize()
+                t = med(lambda: model.forward_boxes(x, masks="u8", out=(st.m, st.b)), args.calls)
+                print(f"[{dtype}] forward_boxes host enqueue {t:.4f} ms (no sync)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -3143,12 +3143,13 @@ hipError_t launch_splitk_reduce(DType to, DType tq, int epi, const IgemmArgs& a,
 // ---------------------------------------------------------------------------------
 // per-(image, field) bounding box of a mask: inference.py:84-90 (np.where(mask) ->
 // xs.min(), xs.max(), ys.min(), ys.max()) on the GPU, 4 ints instead of H*W host bytes.
-// One block per (n, c).  The mask is walked as 16-pixel column words (bit j of word w = pixel
-// 16*w + j: a little-endian 16-bit word of a bit-packed mask, or 16 bytes of a uint8 mask
-// reduced to their nonzero bits); thread t takes words t, t + 256, ..., so with W / 16 dividing
-// 256 it always sees the same column word and ORs it in a register (one LDS atomic per thread
-// instead of one per set pixel), and keeps the first / last row with a set bit.  Four loads are
-// in flight per thread.  Empty mask -> (-1,-1,-1,-1).
+// One 1024-thread block per (n, c).  The mask is walked as 16-pixel column words (bit j of word
+// w = pixel 16*w + j: a little-endian 16-bit word of a bit-packed mask, or 16 bytes of a uint8
+// mask reduced to their nonzero bits); thread t takes words t, t + 1024, ..., so with W / 16
+// dividing 1024 it always sees the same column word and ORs it in a register (one LDS atomic per
+// thread instead of one per set pixel), and keeps the first / last row with a set bit.  Eight
+// loads are in flight per thread: a 512x512 uint8 plane is two rounds of memory latency (with 256
+// threads and four loads it was sixteen, 29 us per batch-1 call).  Empty mask -> (-1,-1,-1,-1).
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ unsigned nz_bits4(unsigned d) {   // bit j = byte j of d nonzero
   d |= d >> 4;
@@ -3157,14 +3158,16 @@ __device__ __forceinline__ unsigned nz_bits4(unsigned d) {   // bit j = byte j o
   return (d & 1u) | ((d >> 7) & 2u) | ((d >> 14) & 4u) | ((d >> 21) & 8u);
 }
 
+constexpr int kBoxThreads = 1024, kBoxLoads = 8;
+
 template <int KIND, bool VEC>
-__global__ __launch_bounds__(256) void mask_boxes_kernel(const uint8_t* __restrict__ masks, int H, int W,
+__global__ __launch_bounds__(kBoxThreads) void mask_boxes_kernel(const uint8_t* __restrict__ masks, int H, int W,
                                                         int* __restrict__ boxes) {
   __shared__ unsigned col_or[kMaxBoxW / 16];
   __shared__ int ymin_s, ymax_s, xmin_s, xmax_s;
   const int tid = threadIdx.x;
   const int words = W / 16;
-  for (int i = tid; i < words; i += 256) col_or[i] = 0u;
+  for (int i = tid; i < words; i += kBoxThreads) col_or[i] = 0u;
   if (tid == 0) { ymin_s = 0x7FFFFFFF; ymax_s = -1; xmin_s = 0x7FFFFFFF; xmax_s = -1; }
   __syncthreads();
   const int total = H * words;
@@ -3184,13 +3187,13 @@ __global__ __launch_bounds__(256) void mask_boxes_kernel(const uint8_t* __restri
   };
   int ymin = 0x7FFFFFFF, ymax = -1, cw = -1;
   unsigned cacc = 0;
-  for (int i0 = tid; i0 < total; i0 += 4 * 256) {
-    unsigned v[4];
+  for (int i0 = tid; i0 < total; i0 += kBoxLoads * kBoxThreads) {
+    unsigned v[kBoxLoads];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = i0 + k * 256 < total ? word_at(i0 + k * 256) : 0u;
+    for (int k = 0; k < kBoxLoads; ++k) v[k] = i0 + k * kBoxThreads < total ? word_at(i0 + k * kBoxThreads) : 0u;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = i0 + k * 256;
+    for (int k = 0; k < kBoxLoads; ++k) {
+      const int i = i0 + k * kBoxThreads;
       if (i >= total) break;
       const int y = i / words, w = i - y * words;
       if (w != cw) {
@@ -3208,7 +3211,7 @@ __global__ __launch_bounds__(256) void mask_boxes_kernel(const uint8_t* __restri
   if (cacc) atomicOr(&col_or[cw], cacc);
   if (ymax >= 0) { atomicMin(&ymin_s, ymin); atomicMax(&ymax_s, ymax); }
   __syncthreads();
-  for (int i = tid; i < words; i += 256) {
+  for (int i = tid; i < words; i += kBoxThreads) {
     const unsigned v = col_or[i];
     if (v) {
       atomicMin(&xmin_s, 16 * i + __builtin_ctz(v));
@@ -3229,7 +3232,7 @@ __global__ __launch_bounds__(256) void mask_boxes_kernel(const uint8_t* __restri
 hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, int H, int W, int* boxes,
                              hipStream_t s) {
   if (W % 16 || W > kMaxBoxW || (kind != MASK_BITS && kind != MASK_U8)) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)(N * ncls)), block(256);
+  const dim3 grid((unsigned)(N * ncls)), block(kBoxThreads);
   if (kind == MASK_BITS) {
     hipLaunchKernelGGL((mask_boxes_kernel<MASK_BITS, false>), grid, block, 0, s, masks, H, W, boxes);
   } else if (reinterpret_cast<uintptr_t>(masks) % 16 == 0) {

@@ -25,10 +25,18 @@ __device__ __forceinline__ int clip8_fixed(int v) {
 }
 }  // namespace
 
+// The tap loops below take the taps eight at a time with all of a group's coefficient and pixel
+// loads issued before the first multiply (the loads are independent; a loop of one tap per
+// iteration waits out a memory latency per tap, 18 us per pass on a 600x400 photo), and the
+// channel count is a template argument so the accumulators stay in registers.  Integer sums are
+// exact, so the grouping does not change a byte.
+constexpr int kTapGroup = 8;
+
 // Horizontal pass: tmp[r][xx][c] = clip8(sum_x src[y0 + r][xmin(xx) + x][c] * kh[xx][x]).
 // One thread per (row, output column), all channels.
+template <int C>
 __global__ __launch_bounds__(256) void resample_h_kernel(const uint8_t* __restrict__ src, int src_stride, int y0,
-                                                        int rows, int C, const int* __restrict__ bounds,
+                                                        int rows, const int* __restrict__ bounds,
                                                         const int* __restrict__ kk, int ksize, int ow,
                                                         uint8_t* __restrict__ tmp) {
   const int xx = blockIdx.x * 256 + threadIdx.x;
@@ -37,18 +45,33 @@ __global__ __launch_bounds__(256) void resample_h_kernel(const uint8_t* __restri
   const int xmin = bounds[2 * xx], n = bounds[2 * xx + 1];
   const int* k = kk + (size_t)xx * ksize;
   const uint8_t* row = src + (size_t)(y0 + r) * src_stride + (size_t)xmin * C;
-  int acc[3] = {1 << (kResamplePrec - 1), 1 << (kResamplePrec - 1), 1 << (kResamplePrec - 1)};
-  for (int x = 0; x < n; ++x) {
-    const int w = k[x];
-    for (int c = 0; c < C; ++c) acc[c] += (int)row[x * C + c] * w;
+  int acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 1 << (kResamplePrec - 1);
+  for (int x0 = 0; x0 < n; x0 += kTapGroup) {
+    int w[kTapGroup], px[kTapGroup][C];
+#pragma unroll
+    for (int j = 0; j < kTapGroup; ++j) {
+      const int t = min(x0 + j, n - 1);   // past the last tap: a valid address, weight 0
+      const int wt = k[t];
+      w[j] = x0 + j < n ? wt : 0;
+#pragma unroll
+      for (int c = 0; c < C; ++c) px[j][c] = (int)row[t * C + c];
+    }
+#pragma unroll
+    for (int j = 0; j < kTapGroup; ++j)
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] += px[j][c] * w[j];
   }
   uint8_t* dst = tmp + ((size_t)r * ow + xx) * C;
+#pragma unroll
   for (int c = 0; c < C; ++c) dst[c] = (uint8_t)clip8_fixed(acc[c]);
 }
 
 // Vertical pass fused with the final conversion: out[c][yy][xx] = clip8(...) / 255 (fp32, the
 // reference's np.float32 division), gray (C = 1) replicated to 3 planes as convert("RGB").
-__global__ __launch_bounds__(256) void resample_v_kernel(const uint8_t* __restrict__ src, int src_stride, int C,
+template <int C>
+__global__ __launch_bounds__(256) void resample_v_kernel(const uint8_t* __restrict__ src, int src_stride,
                                                         const int* __restrict__ bounds, const int* __restrict__ kk,
                                                         int ksize, int oh, int ow, float* __restrict__ out) {
   const int xx = blockIdx.x * 256 + threadIdx.x;
@@ -57,12 +80,26 @@ __global__ __launch_bounds__(256) void resample_v_kernel(const uint8_t* __restri
   const int ymin = bounds[2 * yy], n = bounds[2 * yy + 1];
   const int* k = kk + (size_t)yy * ksize;
   const uint8_t* col = src + (size_t)ymin * src_stride + (size_t)xx * C;
-  int acc[3] = {1 << (kResamplePrec - 1), 1 << (kResamplePrec - 1), 1 << (kResamplePrec - 1)};
-  for (int y = 0; y < n; ++y) {
-    const int w = k[y];
-    for (int c = 0; c < C; ++c) acc[c] += (int)col[(size_t)y * src_stride + c] * w;
+  int acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 1 << (kResamplePrec - 1);
+  for (int y0 = 0; y0 < n; y0 += kTapGroup) {
+    int w[kTapGroup], px[kTapGroup][C];
+#pragma unroll
+    for (int j = 0; j < kTapGroup; ++j) {
+      const int t = min(y0 + j, n - 1);
+      const int wt = k[t];
+      w[j] = y0 + j < n ? wt : 0;
+#pragma unroll
+      for (int c = 0; c < C; ++c) px[j][c] = (int)col[(size_t)t * src_stride + c];
+    }
+#pragma unroll
+    for (int j = 0; j < kTapGroup; ++j)
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] += px[j][c] * w[j];
   }
   const size_t plane = (size_t)oh * ow, o = (size_t)yy * ow + xx;
+#pragma unroll
   for (int c = 0; c < 3; ++c) out[c * plane + o] = (float)clip8_fixed(acc[C == 3 ? c : 0]) / 255.0f;
 }
 
@@ -84,14 +121,21 @@ hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int C, uin
   int stride = p.iw * C;
   if (p.need_h) {
     const dim3 grid((unsigned)((p.ow + 255) / 256), (unsigned)p.h_rows);
-    hipLaunchKernelGGL(resample_h_kernel, grid, dim3(256), 0, s, img, p.iw * C, p.h_y0, p.h_rows, C, p.h_bounds,
-                       p.h_kk, p.h_ksize, p.ow, tmp);
+    if (C == 3)
+      hipLaunchKernelGGL(resample_h_kernel<3>, grid, dim3(256), 0, s, img, p.iw * C, p.h_y0, p.h_rows, p.h_bounds,
+                         p.h_kk, p.h_ksize, p.ow, tmp);
+    else
+      hipLaunchKernelGGL(resample_h_kernel<1>, grid, dim3(256), 0, s, img, p.iw * C, p.h_y0, p.h_rows, p.h_bounds,
+                         p.h_kk, p.h_ksize, p.ow, tmp);
     src = tmp;
     stride = p.ow * C;
   }
   const dim3 grid((unsigned)((p.ow + 255) / 256), (unsigned)p.oh);
-  if (p.need_v)
-    hipLaunchKernelGGL(resample_v_kernel, grid, dim3(256), 0, s, src, stride, C, p.v_bounds, p.v_kk, p.v_ksize, p.oh,
+  if (p.need_v && C == 3)
+    hipLaunchKernelGGL(resample_v_kernel<3>, grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize, p.oh,
+                       p.ow, out);
+  else if (p.need_v)
+    hipLaunchKernelGGL(resample_v_kernel<1>, grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize, p.oh,
                        p.ow, out);
   else
     hipLaunchKernelGGL(to_planar_f32_kernel, grid, dim3(256), 0, s, src, stride, C, p.oh, p.ow, out);
