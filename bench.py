@@ -318,11 +318,12 @@ class StandinRunner:
         return segment
 
 
-def make_leg(runner, rank, world, n_total, per_rank, seed, S, C, dev, chunk):
+def make_leg(runner, rank, world, n_total, per_rank, seed, S, C, dev, chunk, collective=None):
     """Buffers of one timed configuration on this rank: its input shard, its mask shard inside the
     preallocated all-gather send buffer, and the step function (forward + the one exchange).  A
     shard larger than ``chunk`` images runs as consecutive forwards of at most ``chunk`` (the
-    workspace is sized for ``chunk``: 194 MB per 512^2 image at 16 bits)."""
+    workspace is sized for ``chunk``: 194 MB per 512^2 image at 16 bits).  ``step(ev)`` records the
+    event pair ``ev`` (when given) around the exchange: the all-gather's own time inside the step."""
     if per_rank is not None:                        # weak scaling: every rank holds per_rank images
         lo, hi = rank * per_rank, (rank + 1) * per_rank
         n_total = world * per_rank
@@ -330,40 +331,54 @@ def make_leg(runner, rank, world, n_total, per_rank, seed, S, C, dev, chunk):
         lo, hi = udist.shard_bounds(n_total, rank, world)
     n_local = hi - lo
     x = torch.from_numpy(gen_pages(seed + rank, max(n_local, 1), S, C)).to(dev)[:n_local]
-    gather = udist.MaskGather(n_total, (3, S, S // 8), torch.uint8, dev, rank=rank, world=world)
+    gather = udist.MaskGather(n_total, (3, S, S // 8), torch.uint8, dev, rank=rank, world=world,
+                              collective=collective)
     segment = runner.segment_fn()
 
-    def step():
-        if n_local <= chunk:     # the library's data-parallel step (tests/test_dist_cpu.py drives it too)
+    def step(ev=None):
+        if n_local <= chunk and ev is None:   # the library's data-parallel step (tests/test_dist_cpu.py drives it too)
             udist.sharded_mask_step(segment, x, gather)
             return
         for i in range(0, n_local, chunk):
             segment(x[i:i + chunk], gather.local[i:i + chunk])
+        if ev is not None:
+            ev[0].record()
         gather()
+        if ev is not None:
+            ev[1].record()
     return {"x": x, "gather": gather, "step": step, "n_total": n_total, "n_local": n_local}
 
 
 def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
     """The bench contract's timing loop (udist.timed_steps): barrier + sync on both sides, the MAX
-    over ranks; optional per-step GPU times (HIP events on this stream) as a diagnostic."""
+    over ranks; optional per-step GPU times (HIP events on this stream) as a diagnostic, and -- when
+    the leg's step runs the collective -- the all-gather's own time per step (events around it)."""
     # no Python garbage collection inside the timed steps (timeit's practice): a collection pass over
     # torch's and numpy's objects pauses the launching thread for milliseconds, and the GPU idles
     gc.collect()
     gc_was_enabled = gc.isenabled()
     gc.disable()
-    ev = None
+    ev = ag = None
+    collective = leg["gather"].collective
     if per_step_events:
         # created and recorded once before the warmup: torch creates the HIP events lazily at their first
         # record, which would otherwise happen inside the timed steps
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
-        for e in ev:
+        if collective:
+            ag = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for e in ev + [e for pair in (ag or ()) for e in pair]:
             e.record()
     for _ in range(warmup):
         leg["step"]()
     marks = iter(ev[1:]) if ev else iter(())
+    ag_marks = iter(ag) if ag else iter(())
 
     def timed_step():
-        leg["step"]()
+        pair = next(ag_marks, None)
+        if pair is None:
+            leg["step"]()
+        else:
+            leg["step"](pair)
         e = next(marks, None)
         if e is not None:
             e.record()
@@ -371,7 +386,7 @@ def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
         sync()
         ev[0].record()
     try:
-        elapsed, host = udist.timed_steps(timed_step, steps, 0, sync=sync, device=dev)
+        elapsed, host = udist.timed_steps(timed_step, steps, 0, sync=sync, device=dev, collective=collective)
     finally:
         if gc_was_enabled:
             gc.enable()
@@ -379,6 +394,8 @@ def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
            "value": leg["n_total"] * steps / elapsed, "host_step_ms": [round(1e3 * t, 3) for t in host]}
     if ev:
         out["step_ms"] = [round(ev[i].elapsed_time(ev[i + 1]), 3) for i in range(steps)]
+    if ag:
+        out["allgather_ms"] = [round(a.elapsed_time(b), 4) for a, b in ag]
     return out
 
 
@@ -413,7 +430,7 @@ def kernel_table(runner, model, x, masks, B, S, C, dtype, traffic_json):
         k["gflop"] = round(k["gflop"], 1)
         k["algo_gb"] = round(k["algo_gb"], 3)
     peak = PEAK_TFLOPS[dtype]
-    traffic, source = None, None
+    traffic, source = None, {}
     if traffic_json == "auto":
         traffic_json = os.path.join(REPO, "profiles", f"pmc_{dtype}_bs{B}" + ("" if S == 512 else f"_{S}") + ".json")
     if traffic_json and os.path.exists(traffic_json):
@@ -422,13 +439,16 @@ def kernel_table(runner, model, x, masks, B, S, C, dtype, traffic_json):
         meta = tj.get("_meta", {})
         from unet_mi355x.native import kernel_sources_sha256
         stamped = meta.get("kernel_sources_sha256")
-        source = {"file": os.path.relpath(traffic_json, REPO), "commit": meta.get("source_commit"),
-                  "collected": meta.get("collected"), "kernel_sources_sha256": stamped,
-                  # do the PMC counters describe the kernels timed here? (None: not stamped, older summary)
+        # scalars (the driver's record keeps roofline's scalar fields): where the PMC bytes come from and
+        # whether they describe the kernels timed here (None: not stamped, an older summary)
+        source = {"traffic_file": os.path.relpath(traffic_json, REPO), "traffic_commit": meta.get("source_commit"),
+                  "traffic_collected": meta.get("collected"), "traffic_kernel_sources_sha256": stamped,
                   "kernel_sources_match": None if stamped is None else stamped == kernel_sources_sha256()}
     roofline = {"bound": "mfma", "kernel": dom_name, "symbol": mangled(dom_name),
                 "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": source,
+                "frac": round(achieved / peak, 4), "traffic": traffic,
+                "traffic_over_algo": round(traffic / (dom["algo_gb"] * 1e9 / dom["launches"]), 3) if traffic else None,
+                **source,
                 "launches_per_step": dom["launches"], "avg_launch_ms": dom["avg_launch_ms"],
                 "gflop_per_launch": round(dom["gflop"] / dom["launches"], 1),
                 "algo_bytes_per_launch": round(dom["algo_gb"] * 1e9 / dom["launches"])}
@@ -441,7 +461,7 @@ def cpu_baseline(args, sd, x, masks, C, S, extra=()):
     cores: batch-1 forward (images/s + the mask IoU of the GPU masks), batch-8 forward, and
     run_unet end to end (model load + resize + forward + masks + crops, inference.py:50-129).
     extra: (name, x [n, C, h, w] CPU, bit-packed GPU masks [n, 3, h, w/8] CPU, GPU dtype) of other
-    legs, whose masks are compared with the oracle's as `<name>_iou_vs_cpu`."""
+    legs, whose masks are compared with the oracle's as `<name>_iou_min` / `_mean` / `_images`."""
     from PIL import Image
     from oracle import unet_oracle as orc
     threads, info = host_cores()
@@ -481,17 +501,21 @@ def cpu_baseline(args, sd, x, masks, C, S, extra=()):
             ref = orc.masks_from_logits(orc.unet_forward(sd_cpu, xe[j:j + 1]).numpy()[0])
             got = np.unpackbits(me.numpy()[j], axis=-1, bitorder="little").astype(bool)
             ie += [orc.mask_iou(got[i], ref[f]) for i, f in enumerate(orc.FIELDS)]
-        more[f"{name}_iou_vs_cpu"] = {"min": round(min(ie), 5), "mean": round(float(np.mean(ie)), 5),
-                                      "images": int(xe.shape[0]), "size": int(xe.shape[-1]), "gpu_dtype": dte}
-    return {**more, "value": round(done / t_bs1, 4), "unit": "images/s", "cores": threads, "kind": "port",
+        more.update({f"{name}_iou_min": round(min(ie), 5), f"{name}_iou_mean": round(float(np.mean(ie)), 5),
+                     f"{name}_iou_images": int(xe.shape[0]), f"{name}_iou_size": int(xe.shape[-1]),
+                     f"{name}_iou_gpu_dtype": dte})
+    # scalars only: the driver's record keeps the scalar fields of cpu_baseline / roofline
+    return {"value": round(done / t_bs1, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{done} of the bench images, batch 1, {S}x{S}, fp32 eager torch (oracle/unet_oracle.py), "
                       f"{threads} threads",
-            "host": info,
+            "host_cpu": info["cpu_model"], "host_os_cpu_count": info["os_cpu_count"],
+            "host_affinity": info["affinity"], "host_cgroup_quota": info["cgroup_quota"],
             "bs8_images_per_s": round(8 / t_bs8, 4),
             "run_unet_s": round(float(np.median(lat)), 3), "model_load_s": round(t_load, 3),
             "run_unet_sample": "600x400 RGB photo, 2 calls, checkpoint re-loaded per call (inference.py:58)",
-            "iou_vs_cpu": {"min": round(min(ious), 5), "mean": round(float(np.mean(ious)), 5),
-                           "images": done, "gpu_dtype": args.dtype}}
+            # the headline's quality: GPU masks of the timed batch against the oracle's (inference.py:72-79)
+            "iou_min": round(min(ious), 5), "iou_mean": round(float(np.mean(ious)), 5), "iou_images": done,
+            "iou_fields": len(ious), "iou_gpu_dtype": args.dtype, **more}
 
 
 def fp32_leg(args, runner, dev):
@@ -637,6 +661,12 @@ def main():
     ap.add_argument("--cfg5-steps", type=int, default=5)
     ap.add_argument("--standin", action="store_true",
                     help="CPU stand-in forward over gloo (tests: the launcher, sharding and timing without a GPU)")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the process group (nccl; gloo with --standin) and run the N > 1 exchange -- "
+                         "RCCL all-gather inside the step, barriers, device MAX all-reduce -- at every world "
+                         "size, world size 1 included (the multi-GPU code path on a one-GPU box)")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="where rank 0 writes the full record (per-kernel tables, per-step times); '' = stderr only")
     ap.add_argument("--traffic-json", default="auto",
                     help="PMC summary (tools/pmc_summary.py output) to fill roofline.traffic; 'auto' = "
                          "profiles/pmc_<dtype>_bs<batch>.json when present (collected by tools/gpu_round.sh)")
@@ -655,17 +685,20 @@ def main():
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a different GPU count",
               file=sys.stderr)
         sys.exit(2)
+    collective = True if args.dist else None      # None: the exchange runs when world > 1
+    if (world > 1 or args.dist) and "MASTER_ADDR" not in os.environ:   # --dist at world 1, no launcher
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     if args.standin:
         dev = torch.device("cpu")
         sync = lambda: None  # noqa: E731
-        if world > 1:
+        if world > 1 or args.dist:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         runner = StandinRunner(args, dev, world)
     else:
         dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)
         sync = torch.cuda.synchronize
-        if world > 1:
+        if world > 1 or args.dist:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)   # RCCL over xGMI
         runner = NativeRunner(args, dev, world)
 
@@ -682,7 +715,7 @@ def main():
     runner.reserve(chunk, S)
 
     main_leg = make_leg(runner, rank, world, args.global_batch, None if strong else args.batch, 1000, S, C, dev,
-                        chunk)
+                        chunk, collective)
     B = main_leg["n_local"]
     if not args.standin and args.weights == "structured":
         runner.recentre(main_leg["x"])
@@ -692,7 +725,7 @@ def main():
     # ---- strong-scaling shapes (same timing protocol, fewer steps)
     strong_out = []
     for name, g, _ in legs_cfg[1:]:
-        leg = make_leg(runner, rank, world, g, None, 3000, S, C, dev, chunk)
+        leg = make_leg(runner, rank, world, g, None, 3000, S, C, dev, chunk, collective)
         t = time_leg(leg, min(args.steps, 10), 2, sync, dev)
         strong_out.append({"global_batch": g, "per_rank_batch": leg["n_local"] if world == 1 else
                            [udist.shard_bounds(g, r, world)[1] - udist.shard_bounds(g, r, world)[0] for r in range(world)],
@@ -725,6 +758,8 @@ def main():
         cpu = cpu_baseline(args, runner.sd, main_leg["x"], main_leg["gather"].local, C, S, extra)
 
     if rank == 0:
+        exchange = main_leg["gather"].collective
+        ag = res.get("allgather_ms")
         out = {
             "metric": METRIC, "value": round(res["value"], 2), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(res["ms_per_step"], 3),
@@ -733,14 +768,46 @@ def main():
             "data": f"synthetic (seeded invoice-like pages, gray x3; '{args.weights}' seeded weights -- "
                     "the trained checkpoint is an LFS pointer)" if not args.standin else "standin (CPU, gloo)",
             "config": {"workload": f"UNet(n_channels={C}, n_classes=3) forward {S}x{S} + fused sigmoid/"
-                                   f"threshold bit-packed masks" + (" + RCCL all-gather" if world > 1 else ""),
+                                   f"threshold bit-packed masks" + (" + RCCL all-gather" if exchange else ""),
                        "global_batch": main_leg["n_total"], "per_gpu_batch": B, "image": S,
-                       "parallelism": f"dp{world}", "precision_plan": PLAN[args.dtype]},
-            "roofline": roofline, "cpu_baseline": cpu, "strong_scaling": strong_out, "fp32": fp32, "cfg5": cfg5,
-            "latency_bs1": lat, "step_ms": res.get("step_ms"), "host_step_ms": res["host_step_ms"],
-            "kernels": kernels, "layer_ms": layer_ms,
+                       "parallelism": f"dp{world}", "exchange": "all_gather_into_tensor" if exchange else None,
+                       "precision_plan": PLAN[args.dtype]},
+            "allgather_ms": round(float(np.mean(ag)), 4) if ag else None,
+            "roofline": roofline, "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        if out["roofline"] is not None and ag:
+            out["roofline"]["allgather_ms"] = out["allgather_ms"]    # the exchange's share of ms_per_step
+        if cpu is not None:    # the secondary legs' headline scalars, where the driver's record keeps them
+            for name, leg in (("fp32", fp32), ("cfg5", cfg5)):
+                if leg:
+                    cpu[f"{name}_images_per_s"] = leg["value"]
+                    cpu[f"{name}_ms_per_step"] = leg["ms_per_step"]
+                    cpu[f"{name}_frac"] = leg["roofline"]["frac"]
+            for dt, l in (lat or {}).items():
+                cpu[f"gpu_run_unet_ms_{dt}"] = l["run_unet_ms"]
+                cpu[f"gpu_forward_bs1_ms_{dt}"] = l["forward_bs1_eager_ms"]
+        # compact summaries of the other legs; the full tables go to the detail record
+        out["strong_scaling"] = strong_out
+        for name, leg in (("fp32", fp32), ("cfg5", cfg5)):
+            out[name] = None if leg is None else {
+                k: leg[k] for k in ("config", "value", "unit", "ms_per_step", "steps", "whole_step_tflops")}
+            if leg:
+                out[name]["roofline"] = {k: leg["roofline"].get(k) for k in
+                                         ("kernel", "achieved", "frac", "traffic", "kernel_sources_match")}
+        out["latency_bs1"] = None if lat is None else {
+            dt: {k: v for k, v in l.items() if k != "forward_bs1_layer_ms"} for dt, l in lat.items()}
+        detail = {"step_ms": res.get("step_ms"), "host_step_ms": res["host_step_ms"], "allgather_ms": ag,
+                  "kernels": kernels, "layer_ms": layer_ms, "fp32": fp32, "cfg5": cfg5, "latency_bs1": lat}
+        line = json.dumps(out)
+        print("bench_detail " + json.dumps(detail), file=sys.stderr, flush=True)
+        if args.detail_out:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(args.detail_out)), exist_ok=True)
+                with open(args.detail_out, "w") as f:
+                    json.dump({"summary": out, "detail": detail}, f)
+            except OSError as e:
+                print(f"bench: could not write {args.detail_out}: {e}", file=sys.stderr)
+        print(line, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

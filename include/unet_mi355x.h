@@ -32,7 +32,8 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 3   /* 2: unet_forward requires unet_reserve; Cfg renumbered; fp16 range check. 3: unet_crop_stats */
+#define UNET_ABI_VERSION 4   /* 2: unet_forward requires unet_reserve; Cfg renumbered; fp16 range check. 3: unet_crop_stats.
+                                 4: unet_launch_label_at, unet_small_batch_limit, unet_photo_graph_create */
 
 /* error codes */
 #define UNET_OK 0
@@ -165,6 +166,19 @@ int unet_num_launches(void);
  * symbol that rocprofv3 reports; "" for a bad index or a slot fused into the previous launch. */
 const char* unet_launch_label(const unet_handle* h, int i);
 
+/* The same for a forward of N x H x W: batches N <= unet_small_batch_limit(h) run the small-batch
+ * plan, whose split layers launch two kernels -- "partial kernel + splitk_reduce_kernel<...>" -- and
+ * whose under-filled layers may run finer row tiles; N = 0 (or N above the limit) gives the
+ * large-batch labels of unet_launch_label.  The string lives until the calling thread's next call. */
+const char* unet_launch_label_at(const unet_handle* h, int i, int N, int H, int W);
+
+/* Largest batch of the small-batch (split-K) plan, 0 when it is off (UNET_MI355X_KSPLIT=0 at
+ * unet_create).  An image's outputs are bitwise the same for every N <= the limit, and for every N
+ * above it; the two regimes agree within the fp32-accumulation tolerance, not bit for bit, so a
+ * caller that must reproduce batch-1 results exactly runs its batches in chunks of at most the limit
+ * (inference.run_unet_batch does). */
+int unet_small_batch_limit(const unet_handle* h);
+
 /* unet_forward, plus HIP-event timing of every launch on the given stream (ms, in the
  * order above, launch_ms[UNET_NUM_LAUNCHES]).  Synchronises on the stream; for
  * measurement only. */
@@ -193,6 +207,19 @@ int unet_graph_create(unet_handle* h, const void* x, int x_layout, int x_dtype,
                       int N, int H, int W, unet_graph** out);
 int unet_graph_launch(unet_graph* g, void* hip_stream);
 int unet_graph_destroy(unet_graph* g);
+
+/* One graph per photo geometry: the whole device part of run_unet (inference.py:58-129) -- the
+ * upload of the pinned host photo (h_img; NULL: the caller fills img), unet_preprocess to size x size
+ * (the graph owns its resize tables and row buffer, so the handle's geometry cache may evict its own
+ * copy), unet_forward_boxes at N = 1 (masks / mask_kind / boxes as there), unet_crop_stats (pad,
+ * rects, sums as there) and the copies of masks, boxes, rects and sums into the pinned host buffers
+ * given (each may be NULL) -- captured once and replayed by unet_graph_launch: one host call and one
+ * stream synchronisation per photo.  Needs unet_reserve(h, 1, size, size) first; stale (UNET_ESTATE at
+ * launch) under the same rules as unet_graph_create's graphs.  Destroy with unet_graph_destroy. */
+int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih, int iw, int channels, float* x,
+                            int size, void* masks, int mask_kind, int32_t* boxes, double pad, int32_t* rects,
+                            uint64_t* sums, void* h_masks, void* h_boxes, void* h_rects, void* h_sums,
+                            unet_graph** out);
 
 /* Multi-GPU data parallelism: one process per GPU, each rank runs
  * unet_forward / unet_forward_boxes on its contiguous shard of the batch, and the one exchange

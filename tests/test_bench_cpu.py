@@ -46,7 +46,7 @@ def test_self_spawn_weak_scaling():
     assert out["n_gpus"] == 2 and out["scaling"] == "weak"
     assert out["config"]["global_batch"] == 8 and out["config"]["per_gpu_batch"] == 4
     assert out["config"]["parallelism"] == "dp2"
-    assert out["value"] > 0 and len(out["host_step_ms"]) == 3
+    assert out["value"] > 0 and out["config"]["exchange"] == "all_gather_into_tensor"
 
 
 def test_self_spawn_strong_scaling_ragged():
@@ -128,3 +128,34 @@ def test_pmc_summary_labels_mangled_and_demangled_names():
         "conv3x3_halo_kernel<float, 1, 4, 8, 2, 3, 0>"
     assert label_of("_ZN4unet20conv3x3_ring8_kernelIDF16bLi8ELi3ELi0ELi3ELi0EDF16bDF16bLi0ELi0EEEvNS_9IgemmArgsE") == \
         "conv3x3_ring8_kernel<__bf16, 8, 3, 0, 3, 0, __bf16, __bf16, 0, 0>"
+
+
+def test_dist_mode_at_world_one_runs_the_exchange(tmp_path):
+    """--dist at world size 1: the process group is initialised (gloo here, nccl on a GPU) and the
+    step runs the N > 1 exchange -- all_gather_into_tensor into a separate receive buffer, barriers
+    and the MAX all-reduce -- so the multi-GPU code path runs on a one-GPU box."""
+    detail = tmp_path / "detail.json"
+    p, lines = _run([sys.executable, BENCH, "--gpus", "1", "--dist", "--batch", "4", "--detail-out", str(detail)]
+                    + SMALL)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["config"]["exchange"] == "all_gather_into_tensor"
+    assert out["config"]["parallelism"] == "dp1"
+    rec = json.loads(detail.read_text())
+    assert rec["summary"]["value"] == out["value"] and len(rec["detail"]["host_step_ms"]) == 3
+    # without --dist nothing is exchanged at world 1
+    p, lines = _run([sys.executable, BENCH, "--gpus", "1", "--batch", "4", "--detail-out", ""] + SMALL)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert json.loads(lines[0])["config"]["exchange"] is None
+
+
+def test_summary_line_is_compact():
+    """The driver keeps the last 8 KB of stdout: the one JSON line must fit with room to spare; the
+    per-kernel tables and per-step times go to the detail record (stderr and --detail-out)."""
+    p, lines = _run([sys.executable, BENCH, "--gpus", "2", "--batch", "2", "--detail-out", ""] + SMALL)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(lines[0]) < 4096
+    out = json.loads(lines[0])
+    assert "kernels" not in out and "step_ms" not in out
+    assert "bench_detail " in p.stderr

@@ -145,3 +145,82 @@ def test_two_ranks_share_one_gpu_gloo_exchange(monkeypatch):
         assert np.array_equal(masks, ref), f"rank {r}'s gathered masks differ from the one-process forward"
         assert n_steps == 2 and elapsed > 0
     assert got[0][1] == got[1][1], "the MAX-over-ranks elapsed time differs between ranks"
+
+
+_WORLD1_SCRIPT = r"""
+import os, sys, json
+import numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, os.path.join(sys.argv[1], "tw-invoice-unet-ocr-llm_amd"))
+sys.path.insert(0, sys.argv[1])
+import bench
+from unet_mi355x import dist as udist, native, synthetic as syn
+from unet_mi355x.model import UNet
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)      # bench.py --dist
+m = UNet(3, 3, compute_dtype="mixed")
+m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in syn.make_state_dict(0, 3, 3, "pretrained").items()})
+m = m.to(dev).eval()
+h = m.native_handle(dev)
+x = torch.from_numpy(syn.invoice_pages(17, 6, 128, 128, 3)).to(dev)
+h.reserve(6, 128, 128)
+stream = torch.cuda.current_stream(dev).cuda_stream
+g = udist.MaskGather(6, (3, 128, 16), torch.uint8, dev, rank=0, world=1, collective=True)
+assert g.out.data_ptr() != g.send.data_ptr()
+g.out.fill_(0xAB)
+seg = lambda xl, ml: h.forward(xl, None, ml, native.MASK_BITS, stream)
+udist.sharded_mask_step(seg, x, g)                   # forward into the send buffer + RCCL all-gather
+ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+t, per = udist.timed_steps(lambda: udist.sharded_mask_step(seg, x, g), 3, 1, torch.cuda.synchronize, dev,
+                           collective=True)          # barriers + the device MAX all-reduce
+torch.cuda.synchronize()
+ref = torch.empty_like(g.send)
+seg(x, ref)
+torch.cuda.synchronize()
+print(json.dumps({"equal": bool(torch.equal(g.out, ref)), "sent_equal": bool(torch.equal(g.send, ref)),
+                  "elapsed": t, "steps": len(per)}))
+dist.destroy_process_group()
+m.close()
+"""
+
+
+def test_world_one_nccl_exchange_equals_forward(tmp_path):
+    """The N > 1 exchange on the one-GPU box: an nccl (RCCL) process group of world size 1 with
+    device_id, the preallocated MaskGather forced to run all_gather_into_tensor into its separate
+    receive buffer, and dist.timed_steps' barriers + device MAX all-reduce.  The gathered masks equal
+    a plain forward bit for bit.  Run in a child process (one process group, one RCCL communicator)."""
+    import json
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = tmp_path / "world1.py"
+    script.write_text(_WORLD1_SCRIPT)
+    p = subprocess.run([sys.executable, str(script), REPO, str(port)], capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["sent_equal"] and out["equal"], out
+    assert out["steps"] == 3 and out["elapsed"] > 0
+
+
+def test_bench_dist_world_one_line(tmp_path):
+    """bench.py --dist --gpus 1 (nccl at world size 1): the line names the exchange and reports the
+    all-gather's own time per step (HIP events around the collective), which is a small share of the
+    step; the detail record holds the per-step all-gather times."""
+    import json
+    import subprocess
+    detail = tmp_path / "detail.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--dist", "--batch", "8",
+                        "--size", "256", "--steps", "4", "--warmup", "2", "--no-cpu-baseline", "--no-latency",
+                        "--no-fp32", "--no-cfg5", "--no-strong", "--detail-out", str(detail)],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=170)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["config"]["exchange"] == "all_gather_into_tensor" and out["n_gpus"] == 1
+    assert out["allgather_ms"] is not None and 0 < out["allgather_ms"] < out["ms_per_step"]
+    assert out["roofline"]["allgather_ms"] == out["allgather_ms"]
+    rec = json.loads(detail.read_text())
+    assert len(rec["detail"]["allgather_ms"]) == 4

@@ -28,15 +28,16 @@ PASSES=("FETCH_SIZE" "WRITE_SIZE"
 profile() {   # profile SUFFIX TRAFFIC_JSON BENCH_ARGS...
   local S=$1 TJ=$2; shift 2
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG$S -o run -- \
-      python3 bench.py --steps 3 --warmup 1 $P "$@" > gpurun_out/prof_bench_$TAG$S.json 2> gpurun_out/prof_$TAG$S.err
+      python3 bench.py --steps 3 --warmup 1 $P --detail-out gpurun_out/prof_bench_$TAG$S.detail.json "$@" \
+      > gpurun_out/prof_bench_$TAG$S.json 2> gpurun_out/prof_$TAG$S.err
   mkdir -p gpurun_out/pmc_$TAG$S
   local i=0
   for grp in "${PASSES[@]}"; do
     i=$((i+1))
     timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/pmc_$TAG$S/pass$i -o run -- \
-        python3 bench.py --steps 1 --warmup 0 --no-layer-profile $P "$@" > gpurun_out/pmc_$TAG$S/pass$i.log 2>&1
+        python3 bench.py --steps 1 --warmup 0 --no-layer-profile $P --detail-out "" "$@" > gpurun_out/pmc_$TAG$S/pass$i.log 2>&1
   done
-  python tools/pmc_summary.py gpurun_out/pmc_$TAG$S --bench-json gpurun_out/prof_bench_$TAG$S.json --commit $COMMIT \
+  python tools/pmc_summary.py gpurun_out/pmc_$TAG$S --bench-json gpurun_out/prof_bench_$TAG$S.detail.json --commit $COMMIT \
       --out gpurun_out/pmc_$TAG$S/summary.json "${SUMARGS[@]}" > gpurun_out/pmc_$TAG$S/summary.txt
   python tools/prof_summary.py gpurun_out/prof_$TAG$S/run_kernel_trace.csv --min-grid 10000 > gpurun_out/prof_$TAG$S/summary.txt
   cp gpurun_out/pmc_$TAG$S/summary.json "profiles/$TJ"
@@ -54,8 +55,9 @@ profile _fp32 pmc_fp32_bs32.json --batch 32 --dtype fp32
 echo fp32 profiles ok
 fi
 [ "$MODE" = "no-bench" ] && exit 0
-timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 --detail-out gpurun_out/bench_$TAG.detail.json \
+    > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 echo bench ok
 timeout -k 10 300 python bench.py --size 1024 --batch 64 --dtype fp16 --steps 5 --warmup 3 --cpu-seconds 10 --no-latency \
-    --no-strong > gpurun_out/bench_${TAG}_cfg5_fp16_1024.json 2> gpurun_out/bench_${TAG}_cfg5.err
+    --no-strong --detail-out gpurun_out/bench_${TAG}_cfg5.detail.json > gpurun_out/bench_${TAG}_cfg5_fp16_1024.json 2> gpurun_out/bench_${TAG}_cfg5.err
 echo bench cfg5 ok

@@ -52,6 +52,12 @@ def load_pass(d):
         did = int(r["Dispatch_Id"])
         rows[did][0] = r["Kernel_Name"]
         rows[did][1][r["Counter_Name"]] = rows[did][1].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    # the pass's own dispatch times (--kernel-trace beside --pmc): the effective clock of the pass
+    for t in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(t)):
+            did = int(r["Dispatch_Id"])
+            if did in rows:
+                rows[did][1]["_wall_ns"] = float(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     return rows
 
 
@@ -64,12 +70,15 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--esize", type=int, default=2)
     ap.add_argument("--bench-json", default=None,
-                    help="bench.py JSON line of the same build: launches it reports as fused_layers issue no dispatch")
+                    help="bench.py detail record (--detail-out) or JSON line of the same build: launches it reports as fused_layers issue no dispatch")
     ap.add_argument("--commit", default=None, help="git commit of the profiled tree (stamped into _meta)")
     a = ap.parse_args()
     labels = ["?"] * len(LAUNCHES)
     if a.bench_json:
-        kern = json.loads(open(a.bench_json).read().strip().splitlines()[-1])["kernels"]
+        txt = open(a.bench_json).read().strip()
+        rec = json.loads(txt) if txt.startswith("{\"summary\"") else json.loads(txt.splitlines()[-1])
+        # bench.py's detail record ({"summary", "detail"}) or an older single-line record with "kernels"
+        kern = rec["detail"]["kernels"] if "detail" in rec else rec["kernels"]
         by_layer = {l: k for k, v in kern.items() for l in v["layers"]}
         fused = {l for v in kern.values() for l in v.get("fused_layers", [])}   # e.g. up1 inside conv2.3
         labels = ["" if e[0] in fused else by_layer.get(e[0], "?") for e in LAUNCHES]
@@ -80,12 +89,16 @@ def main():
         if not os.path.isdir(p):
             continue
         rows = load_pass(p)
+        have_grbm = any("GRBM_GUI_ACTIVE" in v[1] for v in rows.values())
         # the forward's own launches: every unet:: kernel except the pre/post-processing ones
         ours = [(did, v) for did, v in sorted(rows.items())
                 if v[0].startswith(("_ZN4unet", "void unet::", "unet::")) and not any(s in v[0] for s in ("mask_boxes", "resample", "nhwc_to_nchw",
                                                                                 "to_planar", "x_to_nchw"))]
         last = ours[-len(launches):]
         for i, (did, (name, ctr)) in enumerate(last):
+            wall = ctr.pop("_wall_ns", None)
+            if have_grbm and wall:
+                per_launch[i]["_wall_ns"] = wall        # the clock pass's time: the clock is its GRBM / 8 / wall
             per_launch[i].update(ctr)
             per_launch[i]["kernel_name"] = name
     print(f"{'launch':14s} {'read_GB':>8s} {'write_GB':>8s} {'algo_GB?':>8s} {'mfma_busy%':>10s} {'lds_conf%':>9s} {'wait_any%':>9s}")
@@ -105,6 +118,9 @@ def main():
         k["hbm_write_bytes"] += wr
         k["gflop"] += flops / 1e9
         k["algo_bytes"] += algo
+        if gui and c.get("_wall_ns"):
+            k["clock_cycles"] += gui / 8             # MI355X_MICROARCH 'DVFS give-back': GRBM_GUI_ACTIVE / 8 XCDs
+            k["clock_ns"] += c["_wall_ns"]
     import time
     from unet_mi355x.native import kernel_sources_sha256
     out = {"_meta": {"source_commit": a.commit, "collected": time.strftime("%Y-%m-%d"), "dir": a.dir,
@@ -116,6 +132,9 @@ def main():
                      "hbm_write_bytes_per_launch": k["hbm_write_bytes"] / n,
                      "gflop_per_launch": k["gflop"] / n,
                      "algo_bytes_per_launch": k["algo_bytes"] / n,
+                     # effective clock of the profiled (SQ) pass: which box speed the counters describe
+                     "clock_ghz": round(k["clock_cycles"] / k["clock_ns"], 3) if k["clock_ns"] else None,
+                     "pmc_pass_ms_per_launch": round(k["clock_ns"] / n / 1e6, 4) if k["clock_ns"] else None,
                      "note": "read = 2 x FETCH_SIZE (gfx950 half-count correction), write = WRITE_SIZE"}
     if a.out:
         json.dump(out, open(a.out, "w"), indent=1)

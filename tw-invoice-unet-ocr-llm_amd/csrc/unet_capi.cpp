@@ -135,18 +135,6 @@ struct unet_handle {
   // (UNET_MI355X_KSPLIT_FORCE="i:ks,...", i = 3x3 layer 0..16 or 17 + ConvTranspose 0..3; 0 = auto)
   int ksplit_max = 32;
   int ksplit_force[21] = {};
-  unsigned xcd_rows = 0;   // bit i: 3x3 layer i walks with XCD-owned row tiles (UNET_MI355X_XCDROWS="i,...")
-  int prio_hi = 0;         // UNET_MI355X_PRIO=1: waves 4-7 of the 8-wave kernels at s_setprio 1 (A/B option)
-  unsigned stagger = 0;     // bit i: 3x3 layer i on the staggered ring (UNET_MI355X_STAGGER="i,..."; A/B option)
-  // the same per launch (UNET_MI355X_PRIO_LAYERS="i,..."; bit i = 3x3 layer i, 17 + j = ConvTranspose j):
-  // on down1.3, down2.0, conv1.3, up4, up3 the network measured −0.2 / −0.4 % in two in-process A/Bs
-  // (profiles/tune_r4h_prio_layers.txt) and +0.3 % in two more (tune_r4i_stagger_rejected.txt, columns 2
-  // and 3): within the noise, so off
-  unsigned prio_mask = 0;
-  // ConvTranspose with Cin <= 256 on the weight-stationary kernel: bitwise the ring's, but +7 % on up2
-  // (its two-slot pixel ring gives one step of DMA cover; profiles/tune_r4f_convt_ws_rejected.txt), so an
-  // A/B option (UNET_MI355X_CONVT_WS=1), off
-  int convt_ws = 0;
   void* part = nullptr;   // the current forward's partial buffer (workspace region Buffers::part)
 };
 
@@ -155,6 +143,10 @@ struct unet_graph {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   unsigned long long generation = 0;
+  // unet_photo_graph_create: the resize tables and row buffer the captured preprocess reads, owned by
+  // the graph (the handle's geometry cache may evict its own copy without staling the graph)
+  ResampleStore rs;
+  uint8_t* pp_tmp = nullptr;
 };
 
 namespace {
@@ -594,6 +586,44 @@ int resample_coeffs(int in_size, int out_size, std::vector<int>& bounds, std::ve
 }
 #pragma clang fp contract(on)
 
+// Pillow's separable BICUBIC tables of one (ih, iw) -> (oh, ow) resize, uploaded (synchronously) into
+// device buffers owned by st (unet_preprocess's geometry cache, or a photo graph).
+int build_resample(int ih, int iw, int oh, int ow, ResampleStore& st) {
+  ResamplePlan& p = st.plan;
+  p.ih = ih; p.iw = iw; p.oh = oh; p.ow = ow;
+  p.need_h = ow != iw;
+  p.need_v = oh != ih;
+  std::vector<int> hb, hk, vb, vk;
+  p.h_ksize = resample_coeffs(iw, ow, hb, hk);
+  p.v_ksize = resample_coeffs(ih, oh, vb, vk);
+  p.h_y0 = 0;
+  p.h_rows = ih;
+  if (p.need_h && p.need_v) {   // the horizontal pass covers only the rows the vertical pass reads
+    p.h_y0 = vb[0];
+    p.h_rows = vb[2 * (oh - 1)] + vb[2 * (oh - 1) + 1] - p.h_y0;
+    for (int i = 0; i < oh; ++i) vb[2 * i] -= p.h_y0;
+  }
+  const std::vector<int>* src[4] = {&hb, &hk, &vb, &vk};
+  const int** dst[4] = {&p.h_bounds, &p.h_kk, &p.v_bounds, &p.v_kk};
+  for (int i = 0; i < 4; ++i) {
+    void* d = nullptr;
+    const size_t bytes = src[i]->size() * sizeof(int);
+    hipError_t e = hipMalloc(&d, bytes);
+    if (e != hipSuccess) {
+      free_resample(st);
+      return fail(UNET_ENOMEM, std::string("resample tables: ") + hipGetErrorString(e));
+    }
+    st.bufs.push_back(d);
+    e = hipMemcpy(d, src[i]->data(), bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      free_resample(st);
+      return fail(UNET_EHIP, std::string("resample tables upload: ") + hipGetErrorString(e));
+    }
+    *dst[i] = static_cast<const int*>(d);
+  }
+  return UNET_OK;
+}
+
 int check_geometry(const unet_handle* h, int N, int H, int W) {
   if (N <= 0 || H <= 0 || W <= 0) return fail(UNET_EINVAL, "N, H, W must be positive");
   if (H % 16 || W % 16)
@@ -606,23 +636,30 @@ int check_geometry(const unet_handle* h, int N, int H, int W) {
 
 const char* tname(DType t) { return t == DType::F32 ? "float" : t == DType::BF16 ? "__bf16" : "_Float16"; }
 
-// "kernel<template args>" of a layer, in the same spelling as the demangled symbol
-std::string layer_label(const unet_handle* h, const Layer& L, int epi) {
+// "kernel<template args>" of a layer, in the same spelling as the demangled symbol.  sp: the
+// small-batch plan's choice for the launch (layer_split): a split layer runs its EPI_PARTIAL kernel and
+// the reduction ("A + B"), finer row tiles the 64-row 8-wave ring / the 128-row ConvTranspose ring.
+std::string layer_label(const unet_handle* h, const Layer& L, int epi, Split sp = Split{}) {
   char buf[160];
-  const int cfg = L.cfg;
-  if (cfg == CFG_TRING_R256 && h->convt_ws && L.dt != DType::F32 && L.cin <= 256) {   // launch_up: Cin <= 8 steps
-    std::snprintf(buf, sizeof buf, "convT_ws_kernel<%s, %s>", tname(L.dt), tname(L.dto));
-  } else if (cfg_is_tring(cfg)) {
+  int cfg = L.cfg;
+  (void)h;
+  if (sp.ks == 1 && sp.rows && cfg == CFG_TRING_R256) cfg = CFG_TRING_R128;   // run_igemm's batch-1 halves
+  if (sp.ks > 1) {   // launch_igemm(..., EPI_PARTIAL) + launch_splitk_reduce
+    Layer P = L;
+    P.dto = P.dtq = L.dt;
+    std::string part = layer_label(h, P, EPI_PARTIAL, Split{1, sp.rows});
+    std::snprintf(buf, sizeof buf, " + splitk_reduce_kernel<%s, %s, %d>", tname(L.dto),
+                  tname(epi == EPI_POOL ? L.dtq : L.dto), epi);
+    return part + buf;
+  }
+  if (cfg_is_tring(cfg)) {
     std::snprintf(buf, sizeof buf, "convT_ring_kernel<%s, 8, %d, %d, %s>", tname(L.dt), cfg == CFG_TRING_R256 ? 4 : 3,
                   cfg == CFG_TRING_R256 ? 2 : 1, tname(L.dto));
-  } else if (cfg == CFG_RING8_R128 && &L >= h->L && &L < h->L + 17 && ((h->stagger >> (&L - h->L)) & 1u) &&
-             epi != EPI_UPFUSE) {   // the staggered ring (launch_3x3)
-    std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, 8, 3, %d, 3, 0, %s, %s, 0, %d>", tname(L.dt), epi,
-                  tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto), kRing8Stagger);
   } else if (cfg_is_ring8(cfg)) {
     const int wst = cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;   // weight-stationary
+    const int rows = (sp.rows && cfg == CFG_RING8_R128) ? sp.rows : cfg_rows(cfg);
     std::snprintf(buf, sizeof buf, "conv3x3_ring8_kernel<%s, %d, %d, %d, %d, %d, %s, %s, %d, 0>", tname(L.dt),
-                  cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), wst, tname(L.dto),
+                  rows / 16, ring_ns(cfg), epi, ring_tps(cfg), wst, tname(L.dto),
                   tname(epi == EPI_POOL ? L.dtq : L.dto), cfg == CFG_RING8_FUSED_IN ? 1 : 0);
   } else if (cfg_is_ring(cfg)) {
     std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %s, %s, %d, %d>", tname(L.dt),
@@ -637,7 +674,9 @@ std::string layer_label(const unet_handle* h, const Layer& L, int epi) {
   return buf;
 }
 
-void build_labels(unet_handle* h) {
+// Labels of every launch slot for a forward of N x H x W (N = 0: the large-batch plan, N > kSmallBatch,
+// whatever the size; otherwise the small-batch plan's choices at that shape, layer_split).
+void build_labels_at(const unet_handle* h, int N, int H, int W, std::string (&out)[UNET_NUM_LAUNCHES]) {
   const int C = h->cfg.n_channels;
   char buf[96];
   const DType t0 = h->L[D1B].dt;
@@ -649,18 +688,23 @@ void build_labels(unet_handle* h) {
   for (int i = 0; i < UNET_NUM_LAUNCHES; ++i) {
     const int id = order[i];
     if (id < 0) {
-      h->labels[i] = cfg_fused_in(h->L[D1B].cfg) ? std::string("x_to_px4_kernel<") + tname(t0) + ">" : buf;
+      out[i] = cfg_fused_in(h->L[D1B].cfg) ? std::string("x_to_px4_kernel<") + tname(t0) + ">" : buf;
       continue;
     }
     if (id >= 100) {   // a fused up1 launches nothing: empty label (tools: its time and work go to conv2.3)
-      h->labels[i] = (id == 103 && h->fuse_up1) ? std::string() : layer_label(h, h->U[id - 100], EPI_UPSCATTER);
+      const int j = id - 100;
+      out[i] = (j == 3 && h->fuse_up1) ? std::string()
+                                       : layer_label(h, h->U[j], EPI_UPSCATTER,
+                                                     layer_split(h, 17 + j, h->U[j], EPI_UPSCATTER, N, H >> kUpLevel[j], W >> kUpLevel[j]));
       continue;
     }
     int epi = id == C1B ? EPI_HEAD : (id == D1B || id == D2B || id == D3B || id == D4B) ? EPI_POOL : EPI_STORE;
     if (id == C2B && h->fuse_up1) epi = EPI_UPFUSE;
-    h->labels[i] = layer_label(h, h->L[id], epi);
+    out[i] = layer_label(h, h->L[id], epi,
+                         layer_split(h, id, h->L[id], epi, N, H >> kLayerLevel[id], W >> kLayerLevel[id]));
   }
 }
+void build_labels(unet_handle* h) { build_labels_at(h, 0, 0, 0, h->labels); }
 
 // "layer:cfg,..." override list (tools/tune.py A/B runs)
 void parse_overrides(const char* ov, int n, int* cfg_out, bool (*ok)(int, int)) {
@@ -796,13 +840,14 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
       c = cfg_is_ring8(c) ? (L.cout == 64 ? CFG_RING8_R64_T9 : CFG_RING8_R128)
                           : (L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128);
     if (c == CFG_RING8_R64_WS && (L.cin != 64 || f32)) c = L.cout == 64 ? CFG_RING8_R64_T9 : CFG_RING8_R128;   // 72 KB of weights max
-    if (c == CFG_RING8_R128 && L.cout == 64) c = CFG_RING8_R64_T9;
+    if (c == CFG_RING8_R128 && (L.cout == 64 || f32)) c = CFG_RING8_R64_T9;   // fp32 128-row 8-wave tiles spill
     if (c == CFG_RING_R64_W12 && f32) c = CFG_RING_R64_T3;   // 16-bit only
     if (cfg_rows(c) > L.cout || (i == C1B && cfg_rows(c) != 64))
       c = ring ? CFG_RING_R64_T3 : CFG_HALO_R64_W8;
     // the LDS-halo family stores its own operand type only: keep it off the mixed plan's seams
     const bool pool = i == D1B || i == D2B || i == D3B || i == D4B;
-    if (cfg_is_halo(c) && (L.dto != L.dt || (pool && L.dtq != L.dt))) c = L.cout == 64 ? CFG_RING_R64_T3 : CFG_RING_R128;
+    if (cfg_is_halo(c) && (L.dto != L.dt || (pool && L.dtq != L.dt))) c = L.cout == 64 || pool ? CFG_RING_R64_T3 : CFG_RING_R128;
+    if (c == CFG_RING_R128 && pool) c = CFG_RING_R64_T3;   // pooled 128-row 4-wave tiles spill: same family, 64 rows
     L.cfg = c;
   }
   for (int i = 0; i < 4; ++i) {
@@ -822,21 +867,6 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
                   u1.dt == c2b.dt && u1.dto == c2b.dto;
   }
   if (const char* ks = std::getenv("UNET_MI355X_KSPLIT")) h->ksplit_max = std::atoi(ks);
-  if (const char* pr = std::getenv("UNET_MI355X_PRIO")) h->prio_hi = std::atoi(pr) != 0;
-  if (const char* cw = std::getenv("UNET_MI355X_CONVT_WS")) h->convt_ws = std::atoi(cw) != 0;
-  auto layer_mask = [](const char* v, int n) {   // "i,j,..." -> bit mask of indices < n
-    unsigned m = 0;
-    for (const char* p = v; p && *p;) {
-      const int li = std::atoi(p);
-      if (li >= 0 && li < n) m |= 1u << li;
-      while (*p && *p != ',') ++p;
-      if (*p == ',') ++p;
-    }
-    return m;
-  };
-  h->xcd_rows = layer_mask(std::getenv("UNET_MI355X_XCDROWS"), 17);          // 3x3 layer indices (A/B runs)
-  if (const char* pl = std::getenv("UNET_MI355X_PRIO_LAYERS")) h->prio_mask = layer_mask(pl, 21);   // + 17..20 = up4..up1
-  h->stagger = layer_mask(std::getenv("UNET_MI355X_STAGGER"), 17);
   if (const char* kf = std::getenv("UNET_MI355X_KSPLIT_FORCE")) {   // "i:ks,..." (A/B runs)
     std::string o(kf);
     size_t pos = 0;
@@ -1031,10 +1061,6 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.tiles_y = (H + cfg_tile_h(L.cfg) - 1) / cfg_tile_h(L.cfg);
   a.n_ct = L.ctot / cfg_rows(L.cfg);
   const int id = (&L >= h->L && &L < h->L + 17) ? (int)(&L - h->L) : 17 + (int)(&L - h->U);
-  a.xcd_rows = id < 17 ? (int)((h->xcd_rows >> id) & 1u) : 0;
-  a.prio_hi = h->prio_hi || ((h->prio_mask >> id) & 1u);
-  a.stagger = id < 17 ? (int)((h->stagger >> id) & 1u) : 0;
-  a.convt_ws = h->convt_ws;
   const Split sp = layer_split(h, id, L, epi, N, H, W);
   int cfg = L.cfg;
   if (sp.ks == 1 && sp.rows) {   // small-batch plan, unsplit: finer row tiles over the layer's packing
@@ -1194,38 +1220,8 @@ int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channel
       h->resample.pop_back();
     }
     ResampleStore st;
-    ResamplePlan& p = st.plan;
-    p.ih = ih; p.iw = iw; p.oh = oh; p.ow = ow;
-    p.need_h = ow != iw;
-    p.need_v = oh != ih;
-    std::vector<int> hb, hk, vb, vk;
-    p.h_ksize = resample_coeffs(iw, ow, hb, hk);
-    p.v_ksize = resample_coeffs(ih, oh, vb, vk);
-    p.h_y0 = 0;
-    p.h_rows = ih;
-    if (p.need_h && p.need_v) {   // the horizontal pass covers only the rows the vertical pass reads
-      p.h_y0 = vb[0];
-      p.h_rows = vb[2 * (oh - 1)] + vb[2 * (oh - 1) + 1] - p.h_y0;
-      for (int i = 0; i < oh; ++i) vb[2 * i] -= p.h_y0;
-    }
-    const std::vector<int>* src[4] = {&hb, &hk, &vb, &vk};
-    const int** dst[4] = {&p.h_bounds, &p.h_kk, &p.v_bounds, &p.v_kk};
-    for (int i = 0; i < 4; ++i) {
-      void* d = nullptr;
-      const size_t bytes = src[i]->size() * sizeof(int);
-      hipError_t e = hipMalloc(&d, bytes);
-      if (e != hipSuccess) {
-        free_resample(st);
-        return fail(UNET_ENOMEM, std::string("resample tables: ") + hipGetErrorString(e));
-      }
-      st.bufs.push_back(d);
-      e = hipMemcpy(d, src[i]->data(), bytes, hipMemcpyHostToDevice);
-      if (e != hipSuccess) {
-        free_resample(st);
-        return fail(UNET_EHIP, std::string("resample tables upload: ") + hipGetErrorString(e));
-      }
-      *dst[i] = static_cast<const int*>(d);
-    }
+    const int rc = build_resample(ih, iw, oh, ow, st);
+    if (rc) return rc;
     h->resample.emplace_front(key, std::move(st));
     it = h->resample.begin();
   }
@@ -1268,6 +1264,18 @@ int unet_num_launches(void) { return UNET_NUM_LAUNCHES; }
 const char* unet_launch_label(const unet_handle* h, int i) {
   if (!h || i < 0 || i >= UNET_NUM_LAUNCHES) return "";
   return h->labels[i].c_str();
+}
+
+const char* unet_launch_label_at(const unet_handle* h, int i, int N, int H, int W) {
+  thread_local std::string labels[UNET_NUM_LAUNCHES];
+  if (!h || i < 0 || i >= UNET_NUM_LAUNCHES || N < 0 || H < 0 || W < 0) return "";
+  build_labels_at(h, N, H, W, labels);
+  return labels[i].c_str();
+}
+
+int unet_small_batch_limit(const unet_handle* h) {
+  if (!h) return fail(UNET_EINVAL, "null handle");
+  return h->ksplit_max > 1 ? kSmallBatch : 0;
 }
 
 int unet_forward_timed(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
@@ -1356,6 +1364,79 @@ int unet_graph_create(unet_handle* h, const void* x, int x_layout, int x_dtype, 
   return UNET_OK;
 }
 
+int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih, int iw, int channels, float* x,
+                            int size, void* masks, int mask_kind, int32_t* boxes, double pad, int32_t* rects,
+                            uint64_t* sums, void* h_masks, void* h_boxes, void* h_rects, void* h_sums,
+                            unet_graph** out) {
+  if (!h || !img || !x || !boxes || !rects || !sums || !out) return fail(UNET_EINVAL, "null argument");
+  if (channels != 1 && channels != 3) return fail(UNET_EINVAL, "channels must be 1 (L) or 3 (RGB)");
+  if (ih <= 0 || iw <= 0 || (long long)ih * iw > (1LL << 30) || size <= 0 || size > 16384)
+    return fail(UNET_EINVAL, "bad image or network size");
+  if (!(pad >= 0.0 && pad < 1.0)) return fail(UNET_EINVAL, "bad pad");
+  if (mask_kind < 0 || mask_kind > 2 || (mask_kind != UNET_MASK_NONE && !masks) || (h_masks && mask_kind == UNET_MASK_NONE))
+    return fail(UNET_EINVAL, "bad masks / mask_kind");
+  int rc = check_geometry(h, 1, size, size);
+  if (rc) return rc;
+  if (!h->loaded) return fail(UNET_ESTATE, "weights not loaded");
+  if (plan(h, 1, size, size).total > h->ws_bytes)
+    return fail(UNET_ESTATE, "workspace too small for (1, size, size): call unet_reserve first");
+  DeviceGuard g(h->cfg.device);
+  unet_graph* gr = new unet_graph();
+  gr->h = h;
+  // the graph's own resize tables and row buffer (allocated and uploaded before the capture)
+  rc = build_resample(ih, iw, size, size, gr->rs);
+  const ResamplePlan& p = gr->rs.plan;
+  const size_t tmp = p.need_h ? (size_t)p.h_rows * size * channels : 0;
+  if (!rc && tmp) {
+    hipError_t e = hipMalloc((void**)&gr->pp_tmp, tmp);
+    if (e != hipSuccess) rc = fail(UNET_ENOMEM, std::string("preprocess buffer: ") + hipGetErrorString(e));
+  }
+  hipStream_t cs = nullptr;
+  if (!rc) {
+    hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+    if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  if (!rc) {
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) {
+      rc = fail(UNET_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
+    } else {
+      h->capturing = true;
+      const size_t img_bytes = (size_t)ih * iw * channels;
+      const int ncls = h->cfg.n_classes;
+      if (h_img) e = hipMemcpyAsync(img, h_img, img_bytes, hipMemcpyHostToDevice, cs);   // the photo upload
+      if (e == hipSuccess) e = launch_resample(p, static_cast<const uint8_t*>(img), channels, gr->pp_tmp, x, cs);
+      if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("photo graph upload / resize: ") + hipGetErrorString(e));
+      if (!rc) rc = forward_impl(h, x, UNET_LAYOUT_NCHW, UNET_IN_F32, nullptr, masks, mask_kind, boxes, 1, size, size, cs, nullptr);
+      if (!rc) {
+        e = launch_crop_stats(static_cast<const uint8_t*>(img), ih, iw, channels, boxes, ncls, size, size, pad, rects,
+                              reinterpret_cast<unsigned long long*>(sums), cs);
+        const size_t mbytes = (size_t)ncls * size * (mask_kind == UNET_MASK_BITS ? size / 8 : size);
+        if (e == hipSuccess && h_masks) e = hipMemcpyAsync(h_masks, masks, mbytes, hipMemcpyDeviceToHost, cs);
+        if (e == hipSuccess && h_boxes) e = hipMemcpyAsync(h_boxes, boxes, (size_t)ncls * 16, hipMemcpyDeviceToHost, cs);
+        if (e == hipSuccess && h_rects) e = hipMemcpyAsync(h_rects, rects, (size_t)ncls * 16, hipMemcpyDeviceToHost, cs);
+        if (e == hipSuccess && h_sums) e = hipMemcpyAsync(h_sums, sums, (size_t)ncls * 8, hipMemcpyDeviceToHost, cs);
+        if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("photo graph crop stats / copies: ") + hipGetErrorString(e));
+      }
+      h->capturing = false;
+      e = hipStreamEndCapture(cs, &gr->graph);
+      if (!rc && e != hipSuccess) rc = fail(UNET_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+      if (!rc) {
+        e = hipGraphInstantiate(&gr->exec, gr->graph, nullptr, nullptr, 0);
+        if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+      }
+    }
+  }
+  if (cs) (void)hipStreamDestroy(cs);
+  if (rc) {
+    (void)unet_graph_destroy(gr);
+    return rc;
+  }
+  gr->generation = h->generation;
+  *out = gr;
+  return UNET_OK;
+}
+
 int unet_graph_launch(unet_graph* gr, void* stream) {
   if (!gr || !gr->exec) return fail(UNET_EINVAL, "null graph");
   unet_handle* h = gr->h;
@@ -1375,6 +1456,8 @@ int unet_graph_destroy(unet_graph* gr) {
   drain(gr->h);
   if (gr->exec) (void)hipGraphExecDestroy(gr->exec);
   if (gr->graph) (void)hipGraphDestroy(gr->graph);
+  free_resample(gr->rs);
+  if (gr->pp_tmp) (void)hipFree(gr->pp_tmp);
   delete gr;
   return UNET_OK;
 }

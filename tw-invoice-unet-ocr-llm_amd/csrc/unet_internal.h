@@ -64,15 +64,6 @@ struct IgemmArgs {
   float* part;
   int ksplit;
   int src_br;   // EPI_PARTIAL on the 8-wave ring: row tile of the weight packing when finer than BR (0 = BR)
-  int convt_ws; // ConvTranspose on CFG_TRING_R256 with Cin <= 256: the weight-stationary kernel (convT_ws_kernel)
-  // 8-wave ring: blocks of one XCD share row tiles (ct = XCD label mod n_ct) instead of pixel tiles,
-  // so an XCD's L2 holds 1/min(8, n_ct) of the layer's weights (and streams every pixel tile's halo)
-  int xcd_rows;
-  // 8-wave kernels: waves 4-7 (the second-dispatched half, each SIMD's arbitration loser) run at
-  // s_setprio 1 for the whole launch (MI355X_MICROARCH 'Two waves per SIMD' item 4; A/B option)
-  int prio_hi;
-  // 3-tap 128-row 8-wave ring: waves 4-7 one tap behind waves 0-3 (the staggered ring, A/B option)
-  int stagger;
 };
 
 struct FirstConvArgs {
@@ -97,7 +88,6 @@ __host__ __device__ constexpr int first_tap_addr(int s) { return (int)((0x885522
 // fp32 path; the 64-byte-row ring family (persistent walkers, double-buffered halo, weight ring;
 // K order chunk32-major / tap-minor) is the 16-bit path; the ConvTranspose ring runs the 2x
 // upsamplers.  Selection per layer: unet_capi.cpp (defaults tuned on MI355X, profiles/tune_r1*).
-constexpr int kRing8Stagger = 9;   // conv3x3_ring8_kernel's variant slot (ABL) of the staggered ring
 enum Cfg : int {
   CFG_HALO_R64_W4 = 0,    // 64 rows x 16x16 pixels, 4 waves, 3 weight slots
   CFG_HALO_R64_W8 = 1,    // 64 rows, 8 waves

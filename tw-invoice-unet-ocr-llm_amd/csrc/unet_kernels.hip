@@ -694,44 +694,6 @@ __device__ __forceinline__ void mfma_taps_astream(f32x4 (&acc)[TC][TP], const ch
   }
 }
 
-// The staggered ring's 3-tap sequence (ring8_body, STG): mfma_taps_astream with two runtime
-// (wave-uniform) switches -- skip0: tap 0's MFMAs are not issued (waves 4-7 in the first step, which
-// has no previous tap); hook_on: hook() runs between tap 0 and tap 1 (waves 4-7 at a tile boundary:
-// tap 0 finishes the last tile, hook() is its epilogue, taps 1-2 start the next one).
-template <typename T, int TC, int TP, typename Mid, typename Hook>
-__device__ __forceinline__ void mfma_taps_stg(f32x4 (&acc)[TC][TP], const char* const (&hs)[3],
-                                              const char* const (&ws)[3], const int (&prow)[TP], bool skip0,
-                                              bool hook_on, Mid mid, Hook hook) {
-  constexpr int NT = 3;
-  frag_t ar[3], fb[2][TP];
-  auto lda = [&](int j) { return *reinterpret_cast<const frag_t*>(ws[j / TC] + (j % TC) * 16 * 64); };
-#pragma unroll
-  for (int p = 0; p < TP; ++p) fb[0][p] = *reinterpret_cast<const frag_t*>(hs[0] + prow[p]);
-  ar[0] = lda(0);
-  ar[1] = lda(1);
-  __builtin_amdgcn_sched_group_barrier(0x100, TP + 2, 0);
-#pragma unroll
-  for (int k = 0; k < NT; ++k) {
-#pragma unroll
-    for (int t = 0; t < TC; ++t) {
-      const int j = k * TC + t;
-      if (j + 2 < NT * TC) ar[(j + 2) % 3] = lda(j + 2);
-      if (k + 1 < NT && t < TP) fb[(k + 1) & 1][t] = *reinterpret_cast<const frag_t*>(hs[k + 1] + prow[t]);
-      const frag_t af = ar[j % 3];
-      if (k > 0 || !skip0) {
-#pragma unroll
-        for (int p = 0; p < TP; ++p)
-          mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, fb[k & 1][p]));
-      }
-      if (j + 2 < NT * TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      if (k + 1 < NT && t < TP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
-      if (j == 1) mid();
-    }
-    if (k == 0 && hook_on) hook();
-  }
-}
-
 // Derived geometry / LDS budget of a halo-kernel instantiation (shared with the launcher).
 template <typename T, int WR, int WPX, int TCW, int NS, int KT>
 struct HaloGeom {
@@ -1556,11 +1518,8 @@ __device__ __forceinline__ void wait_vm_barrier_rt(int n) {
 // the prologue's bytes); 5 = no tile epilogue (the accumulators are kept
 // alive, nothing is stored) -- the per-tile epilogue's share of a layer, wrong outputs by construction;
 // 6 = the epilogue's arithmetic without its stores; 7 = its stores (zeros) without the arithmetic.
-// ABL = kRing8Stagger (9): the staggered 3-tap 128-row ring (product, an A/B option; see below) --
-// a variant in the ablation parameter's slot, so that the default ring's code and symbol stay as they are
 template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a) {
-  constexpr int STG = ABL == kRing8Stagger;
   using G = Ring8Geom<T, TCW, NS, TPS, WST, HS>;
   constexpr int NW = G::NW, TW = G::TW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
   constexpr int HWD = G::HWD, HP = G::HP, HI = G::HI, HALO_BYTES = G::HALO_BYTES;
@@ -1591,20 +1550,12 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar: the DMA addresses stay in SGPRs
-  if (a.prio_hi && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const uint32_t lds0 = lds_addr_of(lds);
   const int lane = tid & 63;
   const int wp = wave;   // all 8 waves split the pixels; each covers all BR rows
 
   int ct, slot;
-  if (a.xcd_rows && (gridDim.x & 7) == 0 && 8 % a.n_ct == 0) {
-    // XCD-owned row tiles (blocks b and b + 8 share an XCD): XCD label x runs row tile x mod n_ct for
-    // a contiguous range of walkers, so its L2 streams n_ct / 8 of the weights -- and re-reads every
-    // pixel tile's halo once per row tile instead of once (bijective: gridDim.x = 8 q = n_ct n_slots)
-    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
-    ct = x % a.n_ct;
-    slot = (x / a.n_ct) * (int)(gridDim.x >> 3) + k;
-  } else {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one pixel-tile walker
+  {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one pixel-tile walker
     const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
     const int b = blockIdx.x, x = b & 7, k = b >> 3;
     const int bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
@@ -1723,13 +1674,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       // compiler had moved the tested pieces out of line, a taken branch each)
       if (PIECES % NW == 0 || j < PIECES) glds16_sv(src + off, wlane, dst + j * 1024);
     }
-  };
-  // STG: taps [k0, k1) of step s (this wave's pieces wave + k NW: piece j is 16 rows of tap j / 8)
-  auto issue_w_taps = [&](int s, int dst_slot, int k0, int k1) {
-    const char* src = wblk + (size_t)s * SLOT;
-    const uint32_t dst = lds0 + WOFF + dst_slot * SLOT;
-#pragma unroll
-    for (int k = k0; k < k1; ++k) glds16_sv(src + (wave + k * NW) * 1024, wlane, dst + (wave + k * NW) * 1024);
   };
   int wq_s = 0, wq_slot = 0;
   auto issue_w = [&]() {
@@ -1896,9 +1840,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   }
   if constexpr (WST) {
     for (int s = 0; s < S; ++s) issue_w_step(s, s);
-  } else if constexpr (STG) {   // W(0), and taps 0-1 of W(1) (its tap 2 is issued in step 0)
-    if (total > 0) issue_w_taps(0, 0, 0, 3);
-    if (total > 1) issue_w_taps(1, 1, 0, 2);
   } else {
 #pragma unroll
     for (int k = 0; k < NS - 1; ++k)
@@ -1917,9 +1858,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     for (int i = tid; i < 4 * 64; i += 64 * NW) headw_s[i] = a.bias2[i];
   if constexpr (WST) {
     wait_vm_barrier<0>();
-  } else if constexpr (STG) {
-    if (total > 1) wait_vm_barrier<2>();
-    else wait_vm_barrier<0>();
   } else {
     const int young = total - 1 < NS - 2 ? total - 1 : NS - 2;   // W(1..NS-2) may stay in flight
     wait_vm_barrier_rt(young * wcnt);
@@ -1997,102 +1935,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
                                                  headw_s, headb_s);
       init_acc_bias(0, TC);
       cur = nxt;
-    }
-    return;
-  }
-  if constexpr (STG) {
-    // Staggered ring (MI355X_MICROARCH 'Two waves per SIMD' item 9): waves 4-7 run one tap behind
-    // waves 0-3 -- in the interval between two barriers, waves 0-3 run taps 0-2 of step g, waves 4-7
-    // tap 2 of step g-1 and taps 0-1 of step g (and the epilogue of a tile that ended at step g-1),
-    // so the two waves of a SIMD are never in the same phase (tile epilogue beside MFMAs, the
-    // first tap's read latency beside the partner's MFMAs).  Same MFMA order per accumulator, so
-    // bitwise the unstaggered ring.  The buffers that waves 4-7 still read one interval longer:
-    // tap 2 of a weight slot (its DMA, W2(g+1), is issued in step g, right after the barrier: it
-    // has one interval of cover, taps 0-1 of W(g+2) keep two) and a chunk's halo buffer (the next
-    // chunk but one is issued at the chunk's second step instead of its first).
-    static_assert(TPS == 3 && NS == 3 && !WST && HS == 0 && !UPF && !PART && TC == 8 && PIECES == 3 * NW,
-                  "staggered ring: the 3-tap 128-row ring");
-    const bool lag = wave >= 4;
-    int tap = 0, hseq = 0, c = 0, item = 0, slot0 = 0;
-    int ptap = 0, phseq = 0, pitem = 0, pslot = 0;
-    bool pend = false;          // step g-1 ended a tile (waves 4-7 run its epilogue in step g)
-    int s1 = 1, s2 = 2;         // tile steps of W(g+1), W(g+2) (S >= 3)
-    int k1 = 1, k2 = 2;         // their slots
-    auto tptr = [&](int hq, int tp, int sl, int dx, const char*& hp, const char*& wp_) {
-      hp = lds + (hq & 1) * HALO_BYTES + (tp * HWD + dx) * 64 + ((q ^ ((px_lane + dx) & 3)) << 4);
-      wp_ = wrow + sl * SLOT + dx * WSLOT;
-    };
-    auto epi_tile = [&](int it) {
-      int n, ty, tx;
-      tile_of(it, n, ty, tx);
-#pragma unroll
-      for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<TO, TQ, TP, EPI, TW, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n, ty * 16,
-                                                 tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h, headw_s, headb_s);
-      init_acc_bias(0, TC);
-    };
-    auto tap1 = [&](const char* hp, const char* wq) {   // one tap, unpipelined (the tile-boundary path)
-      frag_t bq[TP];
-#pragma unroll
-      for (int p = 0; p < TP; ++p) bq[p] = *reinterpret_cast<const frag_t*>(hp + prow[p]);
-#pragma unroll
-      for (int t = 0; t < TC; ++t) {
-        const frag_t af = *reinterpret_cast<const frag_t*>(wq + t * 16 * 64);
-#pragma unroll
-        for (int p = 0; p < TP; ++p) mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
-      }
-    };
-    for (int g = 0; g < total; ++g) {
-      const bool hiss = tap == 1 && hseq + 1 < hseq_end;
-      const bool w01 = g + 2 < total;
-      if (g + 1 < total) issue_w_taps(s1, k1, 2, 3);   // W2(g+1): needed at this step's barrier
-      auto dma = [&]() {
-        if (w01) issue_w_taps(s2, k2, 0, 2);
-        if (hiss) issue_halo();
-      };
-      {
-        const char* hs3[3];
-        const char* ws3[3];
-        // waves 4-7: tap 2 of step g-1, taps 0-1 of step g (uniform selects: ONE call site -- a second
-        // tap sequence in the loop, or a peeled first step, makes the compiler spill)
-        const int h0 = lag ? phseq : hseq, t0 = lag ? ptap : tap, l0 = lag ? pslot : slot0;
-        tptr(h0, t0, l0, lag ? 2 : 0, hs3[0], ws3[0]);
-        tptr(hseq, tap, slot0, lag ? 0 : 1, hs3[1], ws3[1]);
-        tptr(hseq, tap, slot0, lag ? 1 : 2, hs3[2], ws3[2]);
-        mfma_taps_stg<T, TC, TP>(acc, hs3, ws3, prow, lag && g == 0, lag && g > 0 && pend, dma,
-                                 [&]() { epi_tile(pitem); });
-      }
-      // W(g+1) landed (and at a chunk end the next halo, issued one step earlier); taps 0-1 of
-      // W(g+2) and a halo issued in this step stay in flight
-      if (w01) {
-        if (hiss) wait_vm_barrier<2 + HI>();
-        else wait_vm_barrier<2>();
-      } else {
-        if (hiss) wait_vm_barrier<HI>();
-        else wait_vm_barrier<0>();
-      }
-      ptap = tap; phseq = hseq; pslot = slot0; pitem = item;
-      pend = false;
-      if (++tap == SPC) {
-        tap = 0;
-        ++hseq;
-        if (++c == nch) {
-          c = 0;
-          pend = true;
-        }
-      }
-      if (pend) {
-        if (!lag) epi_tile(item);
-        ++item;
-      }
-      slot0 = k1; k1 = k2; k2 = k2 == 2 ? 0 : k2 + 1;
-      s1 = s2; s2 = s2 + 1 == S ? 0 : s2 + 1;
-    }
-    if (lag && total > 0) {   // tap 2 of the last step, and the last tile's epilogue
-      const char *hp, *wq;
-      tptr(phseq, ptap, pslot, 2, hp, wq);
-      tap1(hp, wq);
-      epi_tile(pitem);
     }
     return;
   }
@@ -2309,7 +2151,6 @@ static hipError_t launch_ring8(const IgemmArgs& a, hipStream_t s) {
   n_slots -= n_slots % KS;          // every walker keeps one K slice (n_mt is a multiple of KS)
   if (n_slots < KS) n_slots = KS;
   if (n_slots > n_mt) n_slots = n_mt;
-  if (ABL == kRing8Stagger && (a.src_br || a.xcd_rows)) return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv3x3_ring8_kernel<T, TCW, NS, EPI, TPS, WST, TO, TQ, HS, ABL>), dim3(a.n_ct * n_slots), dim3(512),
                      0, s, a);
   return hipGetLastError();
@@ -2346,7 +2187,6 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const uint32_t lds0 = lds_addr_of(lds);
   const int wr = wave >> 2, wp = wave & 3;   // row group (WRW = 2), pixel group
-  if (WRW == 2 && a.prio_hi && wave >= 4) __builtin_amdgcn_s_setprio(1);
   int bid;
   {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one walker
     const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
@@ -2489,160 +2329,6 @@ __global__ __launch_bounds__(256 * WRW, WRW == 1 ? 2 : 1) void convT_ring_kernel
       ++item;
     }
   }
-}
-
-// ConvTranspose2d with the row tile's weights resident in LDS (weight-stationary, round 4): for
-// Cin <= 256 (up2; up1 when it is not fused into conv2.3) the 256-row tile's whole K -- at most 8
-// steps x 16 KB -- fits beside a two-slot pixel ring (2 x 16 KB; 160 KiB in all), so only the input
-// pixels stream: 16 KB of LDS-DMA per step instead of the both-streamed ring's 32 KB.  That ring
-// moves ~32 GB/s per CU of loads + scatter stores on up2 (MFMA 28-33 % busy, HBM 4.3 TB/s), the
-// per-CU LDS-DMA rate the guide measures (MI355X_MICROARCH 'ldsdma-fill').  Same tile, K order,
-// fragment layouts and swizzles as convT_ring_kernel<T, 8, 4, 2>, accumulators starting at the bias
-// (held in registers here: the LDS is full), so the two agree bit for bit.  One step of DMA cover:
-// the next step's pixels are issued under the current step's first MFMAs.
-template <typename T, typename TO>
-__global__ __launch_bounds__(512, 1) void convT_ws_kernel(const IgemmArgs a) {
-  constexpr int NW = 8, TC = 8, TP = 4, BR = 256, BKE = 64 / (int)sizeof(T), SMAX = 8;
-  constexpr int WI = BR / (16 * NW);          // A DMA instructions per wave and step (prologue only)
-  constexpr int BI = 256 / (16 * NW);         // B DMA instructions per wave and step
-  constexpr int ASTEP = BR * 64, BSLOT = 256 * 64, BOFF = SMAX * ASTEP;
-  __shared__ __attribute__((aligned(16))) char lds[BOFF + 2 * BSLOT];
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const uint32_t lds0 = lds_addr_of(lds);
-  const int wr = wave >> 2, wp = wave & 3;   // row group, pixel group
-  int bid;
-  {  // XCD-contiguous remap; consecutive ids = the n_ct row tiles of one walker
-    const int nb = gridDim.x, q = nb >> 3, r = nb & 7;
-    const int b = blockIdx.x, x = b & 7, k = b >> 3;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-  }
-  const int ct = bid % a.n_ct;
-  const int slot = bid / a.n_ct;
-  const int n_slots = gridDim.x / a.n_ct;
-  const int n_mt = a.N * a.tiles_y * a.tiles_x;
-  if (slot >= n_mt) return;
-  const int items = (n_mt - slot + n_slots - 1) / n_slots;
-  const int H = a.H, W = a.W;
-  const int S = a.Cin / BKE;                  // <= SMAX (launcher)
-  const int total = items * S;
-  const char* in = reinterpret_cast<const char*>(a.in);
-  const char* zero = reinterpret_cast<const char*>(a.zero);
-  auto tile_of = [&](int i, int& n, int& ty, int& tx) {
-    int mt = slot + i * n_slots;
-    tx = mt % a.tiles_x;
-    mt /= a.tiles_x;
-    ty = mt % a.tiles_y;
-    n = mt / a.tiles_y;
-  };
-  // prologue: the row tile's weights, all S steps (the ring kernel's packing, [ct][s][256 rows][64 B])
-  {
-    const char* wct = reinterpret_cast<const char*>(a.wgt) + (size_t)ct * S * ASTEP + wave * WI * 1024;
-    const uint32_t wlane = (lane >> 2) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
-    for (int st = 0; st < S; ++st)
-#pragma unroll
-      for (int j = 0; j < WI; ++j)
-        glds16_sv(wct + (size_t)st * ASTEP + j * 1024, wlane, lds0 + st * ASTEP + (wave * WI + j) * 1024);
-  }
-  // pixel stream: per-lane pointers set at a tile's first step (the zero page for pixels outside the
-  // image), + c * 64 B per step, as in convT_ring_kernel
-  int iss_c = 0, iss_i = 0, iss_slot = 0;
-  const char* bsrc[BI];
-  auto issue_b = [&]() {
-    if (iss_c == 0) {
-      int n, ty, tx;
-      tile_of(iss_i, n, ty, tx);
-#pragma unroll
-      for (int j = 0; j < BI; ++j) {
-        const int r = (wave * BI + j) * 16 + (lane >> 2), py = r >> 4, px = r & 15;
-        const int iy = ty * 16 + py, ix = tx * 16 + px;
-        const int chk = ((lane & 3) ^ ((py & 1) << 1)) << 4;
-        const bool ok = iy < H && ix < W;
-        bsrc[j] = ok ? in + ((long long)(n * H + iy) * W + ix) * a.ldi * (long long)sizeof(T) + chk : zero + chk;
-      }
-    }
-    const uint32_t Bs = lds0 + BOFF + iss_slot * BSLOT;
-#pragma unroll
-    for (int j = 0; j < BI; ++j) glds16_s(bsrc[j] + iss_c * BKE * (int)sizeof(T), Bs + (wave * BI + j) * 1024);
-    iss_slot ^= 1;
-    if (++iss_c == S) { iss_c = 0; ++iss_i; }
-  };
-  issue_b();
-  // the accumulators start at the bias: the lane's rows wr*128 + 64 (t / 4) + 16 q + 4 (t % 4) + e
-  const int col = lane & 15, q = lane >> 4;
-  f32x4 bv[TC];
-#pragma unroll
-  for (int t = 0; t < TC; ++t)
-    bv[t] = *reinterpret_cast<const f32x4*>(a.bias + ct * BR + wr * 16 * TC + 64 * (t / 4) + 16 * q + 4 * (t % 4));
-  f32x4 acc[TC][TP];
-  auto init_acc = [&]() {
-#pragma unroll
-    for (int t = 0; t < TC; ++t)
-#pragma unroll
-      for (int p = 0; p < TP; ++p) acc[t][p] = bv[t];
-  };
-  init_acc();
-  int prow[TP];
-#pragma unroll
-  for (int p = 0; p < TP; ++p) {
-    int py, px;
-    pix_of((wp * TP + p) * 16 + col, py, px);
-    prow[p] = (py * 16 + px) * 64 + ((q ^ ((py & 1) << 1)) << 4);
-  }
-  const int wrow = (wr * 16 * TC + col) * 64 + ((q ^ ((col >> 1) & 3)) << 4);
-  wait_vm_barrier<0>();   // weights and step 0's pixels landed (the bias loads too)
-
-  int c = 0, item = 0;
-  for (int g = 0; g < total; ++g) {
-    const bool dma = g + 1 < total;
-    const char* As = lds + c * ASTEP + wrow;
-    const char* Bs = lds + BOFF + (g & 1) * BSLOT;
-    frag_t bq[TP], ar[3];
-#pragma unroll
-    for (int p = 0; p < TP; ++p) bq[p] = *reinterpret_cast<const frag_t*>(Bs + prow[p]);
-    ar[0] = *reinterpret_cast<const frag_t*>(As);
-    ar[1] = *reinterpret_cast<const frag_t*>(As + 16 * 64);
-    __builtin_amdgcn_sched_group_barrier(0x100, TP + 2, 0);
-#pragma unroll
-    for (int t = 0; t < TC; ++t) {
-      if (t + 2 < TC) ar[(t + 2) % 3] = *reinterpret_cast<const frag_t*>(As + (t + 2) * 16 * 64);
-      const frag_t af = ar[t % 3];
-#pragma unroll
-      for (int p = 0; p < TP; ++p)
-        mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af), __builtin_bit_cast(uint4, bq[p]));
-      if (t + 2 < TC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
-      // the next step's pixels into the other slot (its last reads were the previous step's, behind
-      // the previous barrier), under this step's first MFMAs
-      if (t == 1 && dma) issue_b();
-    }
-    // step g+1's pixels landed (the only load in flight; older scatter stores are waited for too)
-    wait_vm_barrier<0>();
-    if (++c == S) {
-      c = 0;
-      int n, ty, tx;
-      tile_of(item, n, ty, tx);
-#pragma unroll
-      for (int h = 0; h < TC / 4; ++h)
-        conv_epilogue<TO, TO, TP, EPI_UPSCATTER, 16, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), n,
-                                                         ty * 16, tx * 16, wp * TP, ct * BR + wr * 16 * TC + 64 * h,
-                                                         nullptr, nullptr, nullptr);
-      init_acc();
-      ++item;
-    }
-  }
-}
-
-template <typename T, typename TO>
-static hipError_t launch_tws(const IgemmArgs& a, hipStream_t s) {
-  constexpr int BKE = 64 / (int)sizeof(T);
-  if (a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 15) / 16) return hipErrorInvalidValue;
-  if (a.Cin % BKE || a.Cin / BKE > 8 || a.Ctot % 256 || a.n_ct != a.Ctot / 256 || a.src_br) return hipErrorInvalidValue;
-  const int n_mt = a.N * a.tiles_y * a.tiles_x;
-  int n_slots = kNumCUs / a.n_ct;   // one 512-thread block per CU (160 KiB of LDS)
-  if (n_slots < 1) n_slots = 1;
-  if (n_slots > n_mt) n_slots = n_mt;
-  hipLaunchKernelGGL((convT_ws_kernel<T, TO>), dim3(a.n_ct * n_slots), dim3(512), 0, s, a);
-  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------
@@ -2876,7 +2562,8 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
     case CFG_HALO_R64_W4: if constexpr (same) return launch_halo<T, 1, 4, 4, 3, EPI, 3>(a, s); break;
     case CFG_HALO_R64_W8: if constexpr (same) return launch_halo<T, 1, 8, 4, 3, EPI, 3>(a, s); break;
     case CFG_HALO_R128: if constexpr (same && EPI != EPI_HEAD) return launch_halo<T, 1, 4, 8, 2, EPI, 3>(a, s); break;
-    case CFG_RING_R128: if constexpr (EPI != EPI_HEAD) return launch_ring<T, 1, 4, 8, 3, EPI, 1, 0, TO, TQ>(a, s); break;
+    // (pooled 128-row 4-wave tiles spill two VGPRs: not built; unet_capi runs those layers on 64-row tiles)
+    case CFG_RING_R128: if constexpr (EPI != EPI_HEAD && EPI != EPI_POOL) return launch_ring<T, 1, 4, 8, 3, EPI, 1, 0, TO, TQ>(a, s); break;
     case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
 #ifdef UNET_ABLATION   // rejected on A/B (profiles/tune_r2j_ring_w12_rejected.txt): ablation builds only
     case CFG_RING_R64_W12:
@@ -2887,9 +2574,9 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
       if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ>(a, s);
       break;
     case CFG_RING8_R128:   // (a.src_br = 128: the batch-1 plan's 64-row tiles over the 128-row packing)
-      if constexpr (EPI != EPI_HEAD) {
+      // 16-bit only: the fp32 128-row 8-wave ring spills (unet_capi runs fp32 on the 64-row ring8 instead)
+      if constexpr (EPI != EPI_HEAD && sizeof(T) == 2) {
         if (a.src_br == 128) return launch_ring8<T, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
-        if (a.stagger && !a.xcd_rows) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ, 0, kRing8Stagger>(a, s);
         return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ>(a, s);
       }
       break;
@@ -2916,10 +2603,7 @@ static hipError_t launch_up(int cfg, const IgemmArgs& a, hipStream_t s) {
       if constexpr (std::is_same<T, TO>::value) return launch_halo<T, 1, 4, 8, 2, EPI_UPSCATTER, 1>(a, s);
       break;
     case CFG_TRING_R128: return launch_tring<T, 8, 3, 1, TO>(a, s);
-    case CFG_TRING_R256:   // Cin <= 256 (up2, an unfused up1): the weight-stationary variant, bitwise the same
-      if constexpr (sizeof(T) == 2)
-        if (a.convt_ws && a.Cin <= 8 * (64 / (int)sizeof(T)) && !a.src_br) return launch_tws<T, TO>(a, s);
-      return launch_tring<T, 8, 4, 2, TO>(a, s);
+    case CFG_TRING_R256: return launch_tring<T, 8, 4, 2, TO>(a, s);
     default: break;
   }
   return hipErrorInvalidValue;

@@ -29,22 +29,30 @@ class MaskGather:
     ``local`` (the first hi - lo rows of a send buffer padded to the largest shard, padding rows
     zero), and ``__call__`` all-gathers the send buffers into ``out`` ([world x cap] rows, rank r's
     shard at rows [r cap, r cap + its size)).  ``rows()`` drops the padding (a copy, outside any
-    timed step).  With "nccl" the collective is RCCL over xGMI; with gloo the same call on CPU."""
+    timed step).  With "nccl" the collective is RCCL over xGMI; with gloo the same call on CPU.
 
-    def __init__(self, n_total: int, row_shape, dtype, device, group=None, rank=None, world=None):
+    ``collective``: None = run the all-gather only when world > 1; True = run it at every world size
+    (bench.py --dist: the N > 1 code path -- RCCL all_gather_into_tensor into a separate receive
+    buffer -- exercised on a one-GPU box)."""
+
+    def __init__(self, n_total: int, row_shape, dtype, device, group=None, rank=None, world=None,
+                 collective=None):
         self.group = group
         self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
         self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
+        self.collective = self.world > 1 if collective is None else bool(collective)
+        if self.collective and not dist.is_initialized():
+            raise RuntimeError("MaskGather(collective=True) needs an initialised process group")
         self.n_total = n_total
         lo, hi = shard_bounds(n_total, self.rank, self.world)
         self.cap = shard_bounds(n_total, 0, self.world)[1]          # largest shard (rank 0)
         self.send = torch.zeros((self.cap,) + tuple(row_shape), dtype=dtype, device=device)
         self.local = self.send[:hi - lo]
-        self.out = self.send if self.world == 1 else \
+        self.out = self.send if not self.collective else \
             torch.empty((self.world * self.cap,) + tuple(row_shape), dtype=dtype, device=device)
 
     def __call__(self) -> torch.Tensor:
-        if self.world > 1:
+        if self.collective:
             dist.all_gather_into_tensor(self.out, self.send, group=self.group)
         return self.out
 
@@ -97,14 +105,16 @@ class ShardedSegmenter:
         return all_gather_rows(masks, n_total, self.group)
 
 
-def timed_steps(step, steps: int, warmup: int, sync=None, device=None, group=None) -> tuple[float, list]:
+def timed_steps(step, steps: int, warmup: int, sync=None, device=None, group=None,
+                collective=None) -> tuple[float, list]:
     """The bench contract's timing loop (bench.py): ``warmup`` untimed steps, then exactly
     ``steps`` timed steps bracketed by a barrier + ``sync()`` on both sides; returns the
     elapsed seconds as the MAX over ranks (one all-reduce on ``device``: the GPU with "nccl",
     the CPU with gloo) and the per-step host times of this rank.  ``step`` runs one step (for
-    N > 1 its forward and the mask all-gather)."""
+    N > 1 its forward and the mask all-gather).  ``collective=True`` runs the barriers and the
+    all-reduce at world size 1 too (bench.py --dist)."""
     sync = sync or (lambda: None)
-    distributed = dist.is_initialized() and dist.get_world_size(group) > 1
+    distributed = dist.is_initialized() and (dist.get_world_size(group) > 1 or bool(collective))
     for _ in range(warmup):
         step()
     if distributed:

@@ -10,12 +10,16 @@ Differences are internal only:
   * the per-field bounding boxes (np.where -> min/max, inference.py:84-90) are computed
     on the GPU too (unet_forward_boxes); the scale / 15 % pad / crop stays on the host;
   * RGB / L photos are resized on the GPU (unet_preprocess, bit-exact with Pillow's
-    BICUBIC resize), so only the original uint8 photo crosses PCIe.
+    BICUBIC resize), so only the original uint8 photo crosses PCIe;
+  * for RGB / L photos the call's device work -- photo upload, resize, forward with masks and
+    boxes, crop statistics and the copies back -- is one hipGraph per photo geometry
+    (unet_photo_graph_create), replayed with one host call and one synchronisation.
 """
 from __future__ import annotations
 
 import os
 import threading
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -138,9 +142,12 @@ def photo_array(pil_img: Image.Image) -> np.ndarray:
 
 
 class _Staging:
-    """Buffers of one cached model's run_unet calls, reused across calls: the photo (pinned host
-    + device), the network input, the u8 masks and boxes (device + pinned host), so a call
-    allocates nothing and makes ONE stream synchronisation (after the two device-to-host copies)."""
+    """Buffers of one device's run_unet calls, reused across calls: the photo (pinned host + device),
+    the network input, the u8 masks and boxes, the crop statistics (device + pinned host), so a call
+    allocates nothing and makes ONE stream synchronisation; and the photo graphs captured over them
+    (one per (model, photo geometry), LRU-bounded), which stay valid while these buffers do."""
+
+    MAX_GRAPHS = 8
 
     def __init__(self, device):
         self.device = torch.device(device)
@@ -155,18 +162,49 @@ class _Staging:
         self.hb = torch.empty(self.b.shape, dtype=torch.int32).pin_memory()
         self.hr = torch.empty(self.r.shape, dtype=torch.int32).pin_memory()
         self.hs = torch.empty(self.s.shape, dtype=torch.int64).pin_memory()
+        self.graphs: OrderedDict = OrderedDict()   # (ih, iw, c) -> (model, native.Graph)
+
+    def stage(self, arr: np.ndarray) -> torch.Tensor:
+        """uint8 [H, W(, C)] host photo -> the pinned host buffer (grown when needed: the photo graphs
+        captured over the old buffers are dropped then).  Returns the device view it is uploaded to."""
+        n = arr.size
+        if self.h_img is None or self.h_img.numel() < n:
+            self.drop_graphs()
+            self.h_img = torch.empty(max(n, 1 << 20), dtype=torch.uint8).pin_memory()
+            self.d_img = torch.empty(self.h_img.numel(), dtype=torch.uint8, device=self.device)
+        self.h_img[:n].numpy()[:] = arr.reshape(-1)
+        return self.d_img[:n].view(arr.shape)
 
     def upload(self, arr: np.ndarray) -> torch.Tensor:
         """uint8 [H, W(, C)] host photo -> device tensor of the same shape (pinned, async)."""
-        n = arr.size
-        if self.h_img is None or self.h_img.numel() < n:
-            self.h_img = torch.empty(max(n, 1 << 20), dtype=torch.uint8).pin_memory()
-            self.d_img = torch.empty(self.h_img.numel(), dtype=torch.uint8, device=self.device)
-        src = self.h_img[:n]
-        src.numpy()[:] = arr.reshape(-1)
-        dst = self.d_img[:n]
-        dst.copy_(src, non_blocking=True)
-        return dst.view(arr.shape)
+        dst = self.stage(arr)
+        dst.view(-1).copy_(self.h_img[:arr.size], non_blocking=True)
+        return dst
+
+    def drop_graphs(self):
+        for _, g in self.graphs.values():
+            g.close()
+        self.graphs.clear()
+
+    def photo_graph(self, model, img: torch.Tensor):
+        """The photo graph of (model, photo geometry): upload + resize + forward (masks, boxes) + crop
+        statistics + copies back (unet_photo_graph_create), captured at the first call of a geometry."""
+        key = tuple(img.shape)
+        e = self.graphs.get(key)
+        if e is not None and e[0] is model:
+            self.graphs.move_to_end(key)
+            return e[1]
+        if e is not None:
+            e[1].close()
+        h = model.native_handle(self.device)
+        h.reserve(1, IMG_SIZE, IMG_SIZE)
+        img3 = img if img.dim() == 3 else img.unsqueeze(-1)
+        g = h.photo_graph(self.h_img, img3, self.x, self.m, native.MASK_U8, self.b, CROP_PAD, self.r, self.s,
+                          self.hm, self.hb, self.hr, self.hs)
+        self.graphs[key] = (model, g)
+        while len(self.graphs) > self.MAX_GRAPHS:
+            self.graphs.popitem(last=False)[1][1].close()
+        return g
 
 
 _staging: dict = {}
@@ -182,40 +220,48 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
         if st is None:
             st = _staging[str(DEVICE)] = _Staging(DEVICE)
     with st.lock, torch.no_grad():
-        img = None
-        if pil_img.mode in ("RGB", "L"):
-            # inference.py:63-64 on the GPU: Pillow-exact BICUBIC resize + convert("RGB") + /255
-            img = st.upload(photo_array(pil_img))
-            model.preprocess(img, IMG_SIZE, out=st.x[0])
-            x = st.x
-        else:   # other PIL modes (RGBA premultiplied resize, P nearest, ...): the reference's host path
-            x = preprocess(pil_img.resize((IMG_SIZE, IMG_SIZE)))      # inference.py:63-64
-        # fused sigmoid + threshold + per-field bounding boxes on the device
-        model.forward_boxes(x, masks="u8", out=(st.m, st.b))
         stream = torch.cuda.current_stream(st.device)
-        if img is not None:   # crop rectangles + near-black test data from the device photo
-            img3 = img if img.dim() == 3 else img.unsqueeze(-1)
-            native.crop_stats(img3, st.b[0], IMG_SIZE, IMG_SIZE, CROP_PAD, st.r, st.s, stream.cuda_stream)
-            st.hr.copy_(st.r, non_blocking=True)
-            st.hs.copy_(st.s, non_blocking=True)
+        if pil_img.mode in ("RGB", "L"):
+            # inference.py:63-64 (Pillow-exact BICUBIC resize + convert("RGB") + /255), the forward with the
+            # fused sigmoid + threshold + per-field boxes, and the crop statistics, all on the device as
+            # one graph per photo geometry: one launch, one synchronisation
+            arr = photo_array(pil_img)
+            img = st.stage(arr)
+            g = st.photo_graph(model, img)
+            try:
+                g.launch(stream.cuda_stream)
+            except RuntimeError:   # stale (the cached model's workspace grew, e.g. run_unet_batch): capture again
+                st.graphs.pop(tuple(img.shape), None)
+                g.close()
+                st.photo_graph(model, img).launch(stream.cuda_stream)
+            stream.synchronize()
+            m = st.hm.numpy()[0].view(np.bool_).copy()   # the kernel writes 0 / 1 bytes
+            rects, sums, ch = st.hr.numpy().copy(), st.hs.numpy().copy(), (3 if arr.ndim == 3 else 1)
+            masks = {k: m[i] for i, k in enumerate(FIELDS)}
+            return masks, {k: crop_from_stats(pil_img, rects[i], sums[i], ch) for i, k in enumerate(FIELDS)}
+        # other PIL modes (RGBA premultiplied resize, P nearest, ...): the reference's host path
+        x = preprocess(pil_img.resize((IMG_SIZE, IMG_SIZE)))      # inference.py:63-64
+        model.forward_boxes(x, masks="u8", out=(st.m, st.b))
         st.hm.copy_(st.m, non_blocking=True)
         st.hb.copy_(st.b, non_blocking=True)
         stream.synchronize()
-        m = st.hm.numpy()[0].view(np.bool_).copy()   # the kernel writes 0 / 1 bytes
+        m = st.hm.numpy()[0].view(np.bool_).copy()
         boxes = st.hb.numpy()[0].copy()
-        if img is not None:
-            rects, sums, ch = st.hr.numpy().copy(), st.hs.numpy().copy(), (3 if img.dim() == 3 else 1)
     masks = {k: m[i] for i, k in enumerate(FIELDS)}
-    if img is None:
-        return masks, boxes_to_crops(pil_img, boxes)
-    return masks, {k: crop_from_stats(pil_img, rects[i], sums[i], ch) for i, k in enumerate(FIELDS)}
+    return masks, boxes_to_crops(pil_img, boxes)
 
 
-def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = None):
-    """Batched run_unet for serving: N photos -> [(masks, crops)] in order, identical per photo
-    to ``run_unet`` (same preprocessing, forward, masks, boxes and crop rules), but one native
-    forward over the whole batch.  RGB / L photos are resized on the GPU straight into their
-    slot of the batch input; other PIL modes take the reference's host resize."""
+def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = None, exact: bool = True):
+    """Batched run_unet for serving: N photos -> [(masks, crops)] in order, with run_unet's
+    preprocessing, forward, masks, boxes and crop rules.  RGB / L photos are resized on the GPU
+    straight into their slot of the batch input; other PIL modes take the reference's host resize.
+
+    exact=True (default): the forward runs in chunks of at most the library's small-batch limit
+    (unet_small_batch_limit, 4), the batches whose outputs are bitwise the same as at N = 1, so every
+    photo's masks and crops are exactly run_unet's.  exact=False: one forward over the whole batch
+    (the large-batch kernels: higher throughput; above the limit the logits agree with run_unet's
+    within the fp32-accumulation tolerance only, so a mask pixel within rounding of its threshold
+    may differ)."""
     model = _cached_model(checkpoint_path, compute_dtype)
     pil_imgs = list(pil_imgs)
     if not pil_imgs:
@@ -227,8 +273,14 @@ def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = N
             model.preprocess(img, IMG_SIZE, out=x[i])
         else:
             x[i] = preprocess(pil.resize((IMG_SIZE, IMG_SIZE)))[0]
+    n = len(pil_imgs)
+    limit = model.native_handle(x.device).small_batch_limit() if exact else 0
+    chunk = limit if limit > 0 else n
+    m = torch.empty((n, len(FIELDS), IMG_SIZE, IMG_SIZE), dtype=torch.uint8, device=x.device)
+    boxes = torch.empty((n, len(FIELDS), 4), dtype=torch.int32, device=x.device)
     with torch.no_grad():
-        m, boxes = model.forward_boxes(x, masks="u8")
+        for i in range(0, n, chunk):
+            model.forward_boxes(x[i:i + chunk], masks="u8", out=(m[i:i + chunk], boxes[i:i + chunk]))
     m = m.cpu().numpy().astype(bool)
     boxes = boxes.cpu().numpy()
     out = []

@@ -122,6 +122,14 @@ class UNet(nn.Module):
         _bump_epoch()
         return out
 
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """nn.Module.load_state_dict; every packed handle re-packs at its next use (also when frozen)."""
+        out = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        with self._lock:
+            self._packed_sig.clear()
+        _bump_epoch()
+        return out
+
     def _signature(self):
         """(data_ptr, _version) of every state_dict tensor: changes on any in-place update
         (load_state_dict, optimizer steps, ``with no_grad(): p.add_``), on .to() / .data
@@ -139,7 +147,10 @@ class UNet(nn.Module):
         idx = device.index if device.index is not None else torch.cuda.current_device()
         with self._lock:
             h = self._handles.get(idx)
-            if h is not None and self._frozen and idx in self._packed_sig:
+            # frozen (the drop-in's private cache): skip the 136-tensor signature while nothing was
+            # re-registered or converted anywhere (_TREE_EPOCH) and no load_state_dict ran (it clears
+            # _packed_sig); otherwise check it as usual
+            if h is not None and self._frozen and idx in self._packed_sig and self._sig_epoch == _TREE_EPOCH[0]:
                 return h
             if h is None:
                 h = native.Handle(self.n_channels, self.n_classes, self.compute_dtype, idx,

@@ -24,7 +24,7 @@ DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16
 MASK_NONE, MASK_U8, MASK_BITS = 0, 1, 2
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
 COMM_ID_BYTES = 128
-ABI_VERSION = 3   # include/unet_mi355x.h UNET_ABI_VERSION
+ABI_VERSION = 4   # include/unet_mi355x.h UNET_ABI_VERSION
 IN_F32, IN_U8 = 0, 1
 
 # every function include/unet_mi355x.h declares: name -> (restype, argtypes)
@@ -52,6 +52,10 @@ SIGNATURES = {
     "unet_crop_stats": (_i, [_vp, _i, _i, _i, _vp, _i, _i, _i, ctypes.c_double, _vp, _vp, _vp]),
     "unet_num_launches": (_i, []),
     "unet_launch_label": (ctypes.c_char_p, [_vp, _i]),
+    "unet_launch_label_at": (ctypes.c_char_p, [_vp, _i, _i, _i, _i]),
+    "unet_small_batch_limit": (_i, [_vp]),
+    "unet_photo_graph_create": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _i, _vp, _i, _vp, ctypes.c_double, _vp, _vp,
+                                     _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
     "unet_forward_timed": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
     "unet_debug_fetch": (_i, [_vp, ctypes.c_char_p, _vp, ctypes.POINTER(_sz), _vp]),
     "unet_graph_create": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _i, ctypes.POINTER(_vp)]),
@@ -255,6 +259,43 @@ class Handle:
         gr = Graph(self, g, (x, logits, masks, boxes))
         self._graphs.add(gr)
         return gr
+
+    def photo_graph(self, h_img: torch.Tensor | None, img: torch.Tensor, x: torch.Tensor, masks: torch.Tensor | None,
+                    mask_kind: int, boxes: torch.Tensor, pad: float, rects: torch.Tensor, sums: torch.Tensor,
+                    h_masks=None, h_boxes=None, h_rects=None, h_sums=None) -> "Graph":
+        """unet_photo_graph_create: upload (pinned ``h_img`` -> ``img``) + preprocess into ``x`` + forward with
+        masks and boxes at N = 1 + crop statistics + copies into the pinned host tensors given, as one
+        graph (run_unet's device work for one photo geometry)."""
+        if img.dtype != torch.uint8 or img.dim() != 3 or not img.is_contiguous():
+            raise ValueError("img must be a contiguous uint8 [H, W, C] device tensor")
+        size = x.shape[-1]
+        if x.dtype != torch.float32 or x.numel() != 3 * size * size or not x.is_contiguous():
+            raise ValueError("x must be a contiguous float32 [1, 3, S, S] device tensor")
+        for t in (h_img, h_masks, h_boxes, h_rects, h_sums):
+            if t is not None and (t.device.type != "cpu" or not t.is_pinned() or not t.is_contiguous()):
+                raise ValueError("host buffers of a photo graph must be contiguous pinned CPU tensors")
+        if h_img is not None and h_img.numel() < img.numel():
+            raise ValueError("h_img is smaller than img")
+        ih, iw, c = img.shape
+        ptr = lambda t: None if t is None else t.data_ptr()   # noqa: E731
+        g = ctypes.c_void_p()
+        with self.lock:
+            check(self.lib.unet_photo_graph_create(self._h, ptr(h_img), img.data_ptr(), ih, iw, c, x.data_ptr(), size,
+                                                   ptr(masks), mask_kind, boxes.data_ptr(), float(pad),
+                                                   rects.data_ptr(), sums.data_ptr(), ptr(h_masks), ptr(h_boxes),
+                                                   ptr(h_rects), ptr(h_sums), ctypes.byref(g)),
+                  "unet_photo_graph_create")
+        gr = Graph(self, g, (h_img, img, x, masks, boxes, rects, sums, h_masks, h_boxes, h_rects, h_sums))
+        self._graphs.add(gr)
+        return gr
+
+    def small_batch_limit(self) -> int:
+        """Largest N of the small-batch (split-K) plan; 0 when it is off (include/unet_mi355x.h)."""
+        return int(self.lib.unet_small_batch_limit(self._h))
+
+    def launch_labels_at(self, n: int, h: int, w: int) -> list:
+        """launch_labels for a forward of n x h x w (the small-batch plan's kernels at n <= its limit)."""
+        return [self.lib.unet_launch_label_at(self._h, i, n, h, w).decode() for i in range(self.lib.unet_num_launches())]
 
     # ---- multi-GPU extras (include/unet_mi355x.h): RCCL all-gather for a host without torch.distributed
     @staticmethod
