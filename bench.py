@@ -359,7 +359,7 @@ def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
     gc_was_enabled = gc.isenabled()
     gc.disable()
     ev = ag = None
-    collective = leg["gather"].collective
+    collective = "gather" in leg and leg["gather"].collective   # the secondary legs have no exchange
     if per_step_events:
         # created and recorded once before the warmup: torch creates the HIP events lazily at their first
         # record, which would otherwise happen inside the timed steps

@@ -33,7 +33,7 @@ extern "C" {
 #endif
 
 #define UNET_ABI_VERSION 4   /* 2: unet_forward requires unet_reserve; Cfg renumbered; fp16 range check. 3: unet_crop_stats.
-                                 4: unet_launch_label_at, unet_small_batch_limit, unet_photo_graph_create */
+                                 4: unet_launch_label_at, unet_small_batch_limit, unet_photo_graph_create, unet_block_* */
 
 /* error codes */
 #define UNET_OK 0
@@ -238,6 +238,28 @@ int unet_allgather(unet_handle* h, const void* send, void* recv, size_t bytes_pe
 int unet_comm_destroy(unet_handle* h);
 
 int unet_destroy(unet_handle* h);
+
+/* Stand-alone DoubleConv block: unet_model.DoubleConv(in_ch, out_ch).forward (unet_model.py:6-20,
+ * conv3x3 + BN + ReLU twice, padding 1) on its own, on the network's kernels: the first-conv kernel
+ * for in_ch 1 or 3 (out_ch 64), the 8-wave MFMA rings (16-bit plans; MIXED = fp16 up to 128 output
+ * channels, bf16 beyond, as the network's levels) or the fp32 LDS-halo kernels.  Supported: in_ch in
+ * {1, 3} with out_ch 64, or in_ch a multiple of 32 with out_ch a multiple of 64 -- every block of the
+ * reference UNet (UNET_ESHAPE otherwise).  Any H, W >= 1.
+ * unet_block_load_weights takes the block's own 14 state_dict keys (net.0.weight, net.0.bias,
+ * net.1.weight / bias / running_mean / running_var / num_batches_tracked, and net.3 / net.4 alike;
+ * BN folded, eps 1e-5).  x / y: device fp32 NCHW [N][in_ch][H][W] / [N][out_ch][H][W]; the workspace
+ * is sized by unet_block_reserve (unet_block_forward never allocates). */
+typedef struct unet_block unet_block;
+typedef struct unet_block_config {
+  int in_ch, out_ch;   /* DoubleConv(in_ch, out_ch) */
+  int dtype;           /* UNET_DTYPE_* */
+  int device;          /* HIP device ordinal */
+} unet_block_config;
+int unet_block_create(const unet_block_config* cfg, unet_block** out);
+int unet_block_load_weights(unet_block* b, const unet_tensor_view* tensors, int n);
+int unet_block_reserve(unet_block* b, int N, int H, int W);
+int unet_block_forward(unet_block* b, const float* x, float* y, int N, int H, int W, void* hip_stream);
+int unet_block_destroy(unet_block* b);
 
 /* Message of the last error on this thread ("" if none). */
 const char* unet_last_error(void);

@@ -126,3 +126,28 @@ def test_photo_array_equals_numpy_view_of_the_photo():
         assert got.dtype == np.uint8 and got.shape == shape and np.array_equal(got, np.asarray(pil)), shape
     rgba = Image.fromarray(rng.integers(0, 256, (5, 7, 4), dtype=np.uint8), "RGBA")
     assert np.array_equal(photo_array(rgba), np.asarray(rgba))
+
+
+def test_doubleconv_standalone_surface_on_cpu():
+    """DoubleConv (unet_model.py:6-20) keeps the reference's 14 state_dict keys; called on its own it
+    runs the native block path, so on CPU it fails loudly (no fallback), checks its channel count,
+    and the library refuses block shapes the native kernels do not cover before touching a GPU."""
+    import ctypes
+    from unet_mi355x import native
+    from unet_mi355x.model import DoubleConv
+    d = DoubleConv(64, 128).eval()
+    assert [k for k in d.state_dict()] == [f"net.{i}.{p}" for i, p in
+                                           [(0, "weight"), (0, "bias"), (1, "weight"), (1, "bias"), (1, "running_mean"),
+                                            (1, "running_var"), (1, "num_batches_tracked"), (3, "weight"), (3, "bias"),
+                                            (4, "weight"), (4, "bias"), (4, "running_mean"), (4, "running_var"),
+                                            (4, "num_batches_tracked")]]
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        d(torch.zeros(1, 64, 8, 8))
+    with pytest.raises(RuntimeError, match="64 channels"):
+        d(torch.zeros(1, 32, 8, 8))
+    assert UNet(3, 3, compute_dtype="mixed").conv2.compute_dtype == "mixed"
+    lib = native.load_library()
+    b = ctypes.c_void_p()
+    for cin, cout in ((5, 64), (3, 128), (64, 96)):
+        rc = lib.unet_block_create(ctypes.byref(native.BlockConfig(cin, cout, 1, 0)), ctypes.byref(b))
+        assert rc == native.UNET_ESHAPE and b"DoubleConv" in lib.unet_last_error(), (cin, cout)

@@ -409,6 +409,23 @@ int check_f16_range(DType dt, const std::vector<double>& w, const std::vector<do
   return UNET_OK;
 }
 
+// The first conv's MFMA operand (first_conv_mfma_kernel): [t][m][16 rows][16 k], packed row
+// rho = 16t + r = natural channel natural_of_packed(rho), k = 4q + c <-> tap first_tap(4m + q) (< 9), channel c
+// (< C); w = the folded [64][C][3][3] weights.
+void pack_first_mfma(DType t0, const std::vector<double>& w, int C, std::vector<uint8_t>& pk) {
+  pk.assign((size_t)4 * 3 * 16 * 16 * 2, 0);
+  for (int rho = 0; rho < 64; ++rho) {
+    const int o = natural_of_packed(rho), tt = rho >> 4, r = rho & 15;
+    for (int m = 0; m < 3; ++m)
+      for (int q = 0; q < 4; ++q) {
+        const int tap = first_tap(4 * m + q);
+        if (tap >= 9) continue;
+        for (int c = 0; c < C; ++c)
+          put_elem(t0, pk, (((size_t)(tt * 3 + m) * 16 + r) * 16 + 4 * q + c), w[(size_t)o * 9 * C + c * 9 + tap]);
+      }
+  }
+}
+
 // 3x3 layer: packed[rho][tap*cin + c] = W'[nat(rho)][c][ky][kx], tap = ky*3+kx
 // Ring kernels (cfg_is_ring) take the same rows in step order instead: per row tile of BR rows,
 // step s = (c / BKE) * 9 + tap holds a contiguous [BR][BKE] block (BKE = 64 bytes of K), so
@@ -926,17 +943,8 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
     const DType t0 = h->L[D1B].dt;
     if (t0 != DType::F32) {   // MFMA operand [t][m][16 rows][16 k] (first_conv_mfma_kernel), packed row
       // rho = 16t + r = natural channel natural_of_packed(rho), k = 4q + c <-> tap first_tap(4m + q) (< 9), channel c (< C)
-      std::vector<uint8_t> pk((size_t)4 * 3 * 16 * 16 * 2, 0);
-      for (int rho = 0; rho < 64; ++rho) {
-        const int o = natural_of_packed(rho), tt = rho >> 4, r = rho & 15;
-        for (int m = 0; m < 3; ++m)
-          for (int q = 0; q < 4; ++q) {
-            const int tap = first_tap(4 * m + q);
-            if (tap >= 9) continue;
-            for (int c = 0; c < C; ++c)
-              put_elem(t0, pk, (((size_t)(tt * 3 + m) * 16 + r) * 16 + 4 * q + c), w[(size_t)o * 9 * C + c * 9 + tap]);
-          }
-      }
+      std::vector<uint8_t> pk;
+      pack_first_mfma(t0, w, C, pk);
       rc = upload(h, &h->w0p, pk.data(), pk.size());
       if (rc) return rc;
       // the ring kernel's fused first conv: [cb][t][m][16 rows][16 k], row (cb, t, r) = channel
@@ -1522,4 +1530,207 @@ int unet_destroy(unet_handle* h) {
   return UNET_OK;
 }
 
+// ---------------------------------------------------------------------------------
+// Stand-alone DoubleConv (unet_model.py:6-20): conv3x3 + BN + ReLU twice on an NCHW fp32 tensor,
+// on the network's own kernels (the first-conv kernel for 1 / 3 input channels, the 8-wave rings on
+// the 16-bit plans, the LDS-halo kernels on fp32), no split-K.
+// ---------------------------------------------------------------------------------
 }  // extern "C"
+
+struct unet_block {
+  unet_handle core;     // allocations, zero page, stream order; the two convs in core.L[0], core.L[1]
+  int cin = 0, cout = 0;
+  bool first = false;   // cin in {1, 3}: conv a is the first-conv kernel (64 outputs)
+};
+
+namespace {
+struct BlockBuffers { size_t in, mid, out, total; };
+BlockBuffers block_plan(const unet_block* b, int N, int H, int W) {
+  const size_t e = dtype_size(b->core.L[1].dt), P = (size_t)N * H * W;
+  BlockBuffers r{};
+  size_t o = 0;
+  r.in = o;
+  if (!b->first) o = align256(o + P * b->cin * e);
+  r.mid = o;
+  o = align256(o + P * b->cout * e);
+  r.out = o;
+  o = align256(o + P * b->cout * e);
+  r.total = o;
+  return r;
+}
+int block_geometry(int N, int H, int W) {
+  if (N <= 0 || H <= 0 || W <= 0) return fail(UNET_EINVAL, "N, H, W must be positive");
+  if ((long long)N * H * W > (1LL << 30)) return fail(UNET_ESHAPE, "N*H*W too large for one call");
+  return UNET_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int unet_block_create(const unet_block_config* cfg, unet_block** out) {
+  if (!cfg || !out) return fail(UNET_EINVAL, "null argument");
+  const int cin = cfg->in_ch, cout = cfg->out_ch;
+  if (cfg->dtype < 0 || cfg->dtype > UNET_DTYPE_MIXED) return fail(UNET_EINVAL, "bad dtype");
+  const bool first = cin == 1 || cin == 3;
+  if (cout <= 0 || cout % 64 || (first && cout != 64) || (!first && (cin <= 0 || cin % 32)))
+    return fail(UNET_ESHAPE, "DoubleConv(in_ch, out_ch) runs natively for in_ch in {1, 3} with out_ch = 64, or in_ch "
+                             "a multiple of 32 and out_ch a multiple of 64 (every block of the reference UNet)");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(UNET_EINVAL, "bad device ordinal");
+  unet_block* b = new unet_block();
+  b->cin = cin;
+  b->cout = cout;
+  b->first = first;
+  unet_handle& h = b->core;
+  h.cfg.n_channels = first ? cin : 3;
+  h.cfg.n_classes = 1;
+  h.cfg.dtype = cfg->dtype;
+  h.cfg.device = cfg->device;
+  h.ksplit_max = 0;
+  const bool f32 = cfg->dtype == UNET_DTYPE_F32;
+  // the mixed plan's storage type at this block's resolution level in the reference network: fp16 up to
+  // 128 channels (levels 0-1), bf16 beyond (levels 2-4)
+  const DType t = f32 ? DType::F32 : cfg->dtype == UNET_DTYPE_F16 ? DType::F16 : cfg->dtype == UNET_DTYPE_BF16 ? DType::BF16
+                : (cout <= 128 ? DType::F16 : DType::BF16);
+  h.dt = f32 ? DType::F32 : DType::BF16;
+  for (int i = 0; i < 2; ++i) {
+    Layer& L = h.L[i];
+    L.cin = i == 0 ? cin : cout;
+    L.cout = L.ctot = cout;
+    L.taps = 9;
+    L.dt = L.dto = L.dtq = t;
+    if (f32) L.cfg = cout == 64 ? CFG_HALO_R64_W8 : CFG_HALO_R128;
+    else L.cfg = cout == 64 ? (L.cin == 64 ? CFG_RING8_R64_WS : CFG_RING8_R64_T9) : CFG_RING8_R128;
+  }
+  DeviceGuard g(cfg->device);
+  hipError_t e = hipEventCreateWithFlags(&h.done, hipEventDisableTiming);
+  if (e != hipSuccess) { delete b; return fail(UNET_EHIP, std::string("hipEventCreate: ") + hipGetErrorString(e)); }
+  std::vector<uint8_t> z(4096, 0);
+  int rc = upload(&h, &h.zero, z.data(), z.size());
+  if (rc) { free_all(&h); (void)hipEventDestroy(h.done); delete b; return rc; }
+  *out = b;
+  return UNET_OK;
+}
+
+int unet_block_load_weights(unet_block* b, const unet_tensor_view* t, int n) {
+  if (!b || (!t && n)) return fail(UNET_EINVAL, "null argument");
+  SD sd;
+  std::vector<std::string> names(n);
+  for (int i = 0; i < n; ++i) {
+    if (!t[i].name) return fail(UNET_EINVAL, "tensor without a name");
+    names[i] = std::string("b.") + t[i].name;   // fold() reads <block>.net.<i>.*
+  }
+  for (int i = 0; i < n; ++i) sd.m[names[i]] = &t[i];
+  if ((int)sd.m.size() != 14)   // net.{0,3}.{weight,bias} + net.{1,4}.{weight,bias,running_mean,running_var,num_batches_tracked}
+    return fail(UNET_EKEY, "DoubleConv state_dict has " + std::to_string(sd.m.size()) + " keys, expected 14");
+  unet_handle& h = b->core;
+  DeviceGuard g(h.cfg.device);
+  drain(&h);
+  ++h.generation;
+  for (void* p : h.allocs)
+    if (p != h.zero) (void)hipFree(p);
+  h.allocs.assign(1, h.zero);
+  h.loaded = false;
+  std::vector<double> w, bb;
+  int rc = fold(sd, "b", "0", b->cin, b->cout, w, bb);
+  if (!rc) rc = check_f16_range(h.L[0].dt, w, bb, "net.0");
+  if (rc) return rc;
+  if (b->first) {
+    std::vector<float> wf(w.begin(), w.end()), bf(bb.begin(), bb.end());
+    rc = upload(&h, (void**)&h.w0, wf.data(), wf.size() * 4);
+    if (!rc) rc = upload(&h, (void**)&h.b0, bf.data(), bf.size() * 4);
+    h.w0p = nullptr;
+    if (!rc && h.L[0].dt != DType::F32) {
+      std::vector<uint8_t> pk;
+      pack_first_mfma(h.L[0].dt, w, b->cin, pk);
+      rc = upload(&h, &h.w0p, pk.data(), pk.size());
+    }
+  } else {
+    rc = pack3x3(&h, h.L[0], w, bb);
+  }
+  if (rc) return rc;
+  rc = fold(sd, "b", "3", b->cout, b->cout, w, bb);
+  if (!rc) rc = check_f16_range(h.L[1].dt, w, bb, "net.3");
+  if (!rc) rc = pack3x3(&h, h.L[1], w, bb);
+  if (rc) return rc;
+  h.loaded = true;
+  return UNET_OK;
+}
+
+int unet_block_reserve(unet_block* b, int N, int H, int W) {
+  if (!b) return fail(UNET_EINVAL, "null block");
+  int rc = block_geometry(N, H, W);
+  if (rc) return rc;
+  unet_handle& h = b->core;
+  const size_t need = block_plan(b, N, H, W).total;
+  if (need <= h.ws_bytes) return UNET_OK;
+  DeviceGuard g(h.cfg.device);
+  ++h.generation;
+  if (h.ws) {
+    drain(&h);
+    (void)hipFree(h.ws);
+    h.ws = nullptr;
+    h.ws_bytes = 0;
+  }
+  hipError_t e = hipMalloc((void**)&h.ws, need);
+  if (e != hipSuccess) {
+    h.ws = nullptr;
+    return fail(UNET_ENOMEM, std::string("block workspace hipMalloc: ") + hipGetErrorString(e));
+  }
+  h.ws_bytes = need;
+  return UNET_OK;
+}
+
+int unet_block_forward(unet_block* b, const float* x, float* y, int N, int H, int W, void* stream) {
+  if (!b || !x || !y) return fail(UNET_EINVAL, "null argument");
+  unet_handle& h = b->core;
+  if (!h.loaded) return fail(UNET_ESTATE, "weights not loaded");
+  int rc = block_geometry(N, H, W);
+  if (rc) return rc;
+  const BlockBuffers B = block_plan(b, N, H, W);
+  if (B.total > h.ws_bytes) return fail(UNET_ESTATE, "workspace too small for this (N, H, W): call unet_block_reserve first");
+  DeviceGuard g(h.cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  order_after_last(&h, s);
+  const DType t = h.L[1].dt;
+  void* mid = h.ws + B.mid;
+  void* outb = h.ws + B.out;
+  hipError_t e = hipSuccess;
+  if (b->first) {
+    FirstConvArgs f{};
+    f.x = x;
+    f.w = h.w0;
+    f.wp = h.w0p;
+    f.b = h.b0;
+    f.out = mid;
+    f.N = N; f.C = b->cin; f.H = H; f.W = W;
+    e = launch_first_conv(t, f, s);
+    if (e != hipSuccess) return fail(UNET_EHIP, std::string("block first conv launch: ") + hipGetErrorString(e));
+  } else {
+    e = launch_nchw_to_nhwc(t, x, N, b->cin, H, W, h.ws + B.in, s);
+    if (e != hipSuccess) return fail(UNET_EHIP, std::string("block input transpose: ") + hipGetErrorString(e));
+    rc = run_igemm(&h, h.L[0], EPI_STORE, h.ws + B.in, N, H, W, b->cin, mid, b->cout, 0, nullptr, 0, s);
+    if (rc) return rc;
+  }
+  rc = run_igemm(&h, h.L[1], EPI_STORE, mid, N, H, W, b->cout, outb, b->cout, 0, nullptr, 0, s);
+  if (rc) return rc;
+  e = launch_nhwc_to_nchw(t, outb, N, b->cout, H, W, y, s);
+  if (e != hipSuccess) return fail(UNET_EHIP, std::string("block output transpose: ") + hipGetErrorString(e));
+  mark_done(&h, s);
+  return UNET_OK;
+}
+
+int unet_block_destroy(unet_block* b) {
+  if (!b) return UNET_OK;
+  {
+    DeviceGuard g(b->core.cfg.device);
+    free_all(&b->core);
+    if (b->core.done) (void)hipEventDestroy(b->core.done);
+  }
+  delete b;
+  return UNET_OK;
+}
+
+}  // extern "C"
+

@@ -137,6 +137,9 @@ hipError_t launch_x_to_px4(DType t, const void* x, int layout, int xdt, int N, i
 hipError_t launch_x_to_nchw_f32(const void* x, int layout, int xdt, int N, int C, int H, int W, float* out,
                                 hipStream_t s);
 // NHWC (pixel stride ld, channel offset choff, C channels) element type t -> NCHW fp32
+// stand-alone DoubleConv (unet_block_*): fp32 NCHW [N][C][H][W] <-> NHWC T [N][H][W][C] (dense)
+hipError_t launch_nchw_to_nhwc(DType t, const float* x, int N, int C, int H, int W, void* out, hipStream_t s);
+hipError_t launch_nhwc_to_nchw(DType t, const void* src, int N, int C, int H, int W, float* y, hipStream_t s);
 hipError_t launch_nhwc_to_nchw_f32(DType t, const void* src, int N, int H, int W, int C, int ld,
                                    int choff, float* dst, hipStream_t s);
 // Pillow-exact separable resize (unet_preprocess.hip): device coefficient tables of one

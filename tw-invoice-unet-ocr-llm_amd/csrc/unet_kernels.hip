@@ -3071,4 +3071,83 @@ hipError_t launch_nhwc_to_nchw_f32(DType t, const void* src, int N, int H, int W
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------
+// layout transposes of the stand-alone DoubleConv (unet_block_*): fp32 NCHW <-> NHWC T through a
+// 32-channel x 64-pixel LDS tile, both sides coalesced (pixels along the NCHW rows, 16-byte channel
+// runs along the NHWC pixels).  HBM-bound.
+// ---------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restrict__ x, int C, int HW, T* __restrict__ out) {
+  __shared__ float tile[32][65];
+  const int n = blockIdx.z, c0 = blockIdx.y * 32, p0 = blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  const float* src = x + (long long)n * C * HW;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {   // rows c0 + 4k + tid / 64, pixel p0 + tid % 64
+    const int c = c0 + 4 * k + (tid >> 6), p = p0 + (tid & 63);
+    tile[4 * k + (tid >> 6)][tid & 63] = (c < C && p < HW) ? src[(long long)c * HW + p] : 0.f;
+  }
+  __syncthreads();
+  const int p = p0 + (tid >> 2), cg = (tid & 3) * 8;   // pixel, 8-channel group
+  if (p >= HW || c0 + cg >= C) return;
+  typedef T t8 __attribute__((ext_vector_type(8)));
+  t8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (T)tile[cg + j][tid >> 2];
+  T* dst = out + ((long long)n * HW + p) * C + c0 + cg;
+  if (c0 + cg + 8 <= C) {
+    *reinterpret_cast<t8*>(dst) = v;
+  } else {
+    for (int j = 0; c0 + cg + j < C; ++j) dst[j] = v[j];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void nhwc_to_nchw_tiled_kernel(const T* __restrict__ src, int C, int HW, float* __restrict__ y) {
+  __shared__ float tile[32][65];
+  const int n = blockIdx.z, c0 = blockIdx.y * 32, p0 = blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  {
+    const int p = p0 + (tid >> 2), cg = (tid & 3) * 8;
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    t8 v = {};
+    if (p < HW && c0 + cg + 8 <= C) {
+      v = *reinterpret_cast<const t8*>(src + ((long long)n * HW + p) * C + c0 + cg);
+    } else if (p < HW) {
+      for (int j = 0; c0 + cg + j < C && j < 8; ++j) v[j] = src[((long long)n * HW + p) * C + c0 + cg + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[cg + j][tid >> 2] = (float)v[j];
+  }
+  __syncthreads();
+  float* dst = y + (long long)n * C * HW;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c0 + 4 * k + (tid >> 6), p = p0 + (tid & 63);
+    if (c < C && p < HW) dst[(long long)c * HW + p] = tile[4 * k + (tid >> 6)][tid & 63];
+  }
+}
+
+hipError_t launch_nchw_to_nhwc(DType t, const float* x, int N, int C, int H, int W, void* out, hipStream_t s) {
+  const int HW = H * W;
+  const dim3 grid((unsigned)((HW + 63) / 64), (unsigned)((C + 31) / 32), (unsigned)N), block(256);
+  switch (t) {
+    case DType::F32: hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, grid, block, 0, s, x, C, HW, (float*)out); break;
+    case DType::BF16: hipLaunchKernelGGL(nchw_to_nhwc_kernel<__bf16>, grid, block, 0, s, x, C, HW, (__bf16*)out); break;
+    case DType::F16: hipLaunchKernelGGL(nchw_to_nhwc_kernel<_Float16>, grid, block, 0, s, x, C, HW, (_Float16*)out); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_nhwc_to_nchw(DType t, const void* src, int N, int C, int H, int W, float* y, hipStream_t s) {
+  const int HW = H * W;
+  const dim3 grid((unsigned)((HW + 63) / 64), (unsigned)((C + 31) / 32), (unsigned)N), block(256);
+  switch (t) {
+    case DType::F32: hipLaunchKernelGGL(nhwc_to_nchw_tiled_kernel<float>, grid, block, 0, s, (const float*)src, C, HW, y); break;
+    case DType::BF16: hipLaunchKernelGGL(nhwc_to_nchw_tiled_kernel<__bf16>, grid, block, 0, s, (const __bf16*)src, C, HW, y); break;
+    case DType::F16: hipLaunchKernelGGL(nhwc_to_nchw_tiled_kernel<_Float16>, grid, block, 0, s, (const _Float16*)src, C, HW, y); break;
+  }
+  return hipGetLastError();
+}
+
 }  // namespace unet

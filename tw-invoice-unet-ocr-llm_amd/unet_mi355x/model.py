@@ -39,14 +39,15 @@ _mm.register_module_module_registration_hook(_bump_epoch)
 
 
 class DoubleConv(nn.Module):
-    """Parameter container matching unet_model.py:6-17 (conv3x3, BN, ReLU) x 2.
+    """unet_model.py:6-20: (conv3x3, BN, ReLU) x 2 -- the same parameters (and state_dict keys).
 
-    The native path executes DoubleConv blocks only inside the whole-network
-    forward (fused with pooling / concat / head), so calling a block on its own is
-    not supported.
+    Inside UNet.forward the blocks run fused with pooling / concat / head (the whole-network native
+    path).  Called on its own, forward runs the block on the native library too (unet_block_*: the
+    first-conv kernel or the MFMA rings, BN folded, eval semantics), for every block shape of the
+    reference network; ``compute_dtype`` as UNet's (None: the UNET_MI355X_DTYPE default, fp32).
     """
 
-    def __init__(self, in_ch: int, out_ch: int):
+    def __init__(self, in_ch: int, out_ch: int, compute_dtype: str | None = None):
         super().__init__()
         self.net = nn.Sequential(
             nn.Conv2d(in_ch, out_ch, kernel_size=3, padding=1),
@@ -56,14 +57,54 @@ class DoubleConv(nn.Module):
             nn.BatchNorm2d(out_ch),
             nn.ReLU(inplace=True),
         )
+        self.in_ch, self.out_ch = in_ch, out_ch
+        self.compute_dtype = compute_dtype
+        self._blocks: dict = {}
+        self._packed_sig: dict = {}
+        self._lock = threading.Lock()
 
-    def forward(self, x):  # pragma: no cover - documented limitation
-        raise RuntimeError("unet_mi355x: DoubleConv runs only inside UNet.forward (fused native path)")
+    def forward(self, x):
+        """unet_model.py:19-20 on the native path: NCHW in -> NCHW fp32 out [N, out_ch, H, W]."""
+        if not isinstance(x, torch.Tensor) or x.dim() != 4:
+            raise RuntimeError("DoubleConv.forward expects a 4-D NCHW tensor")
+        if x.shape[1] != self.in_ch:
+            raise RuntimeError(f"expected input with {self.in_ch} channels, got {x.shape[1]}")
+        if x.device.type != "cuda":
+            raise RuntimeError("unet_mi355x: DoubleConv runs only on a ROCm GPU tensor "
+                               f"(got device {x.device}); there is no CPU fallback")
+        if self.training and torch.is_grad_enabled():
+            raise RuntimeError("unet_mi355x.DoubleConv is inference-only (eval BatchNorm folded, no autograd); "
+                               "call .eval() or run under torch.no_grad()")
+        dtype = self.compute_dtype or DEFAULT_DTYPE
+        idx = x.device.index if x.device.index is not None else torch.cuda.current_device()
+        with self._lock:
+            blk = self._blocks.get((idx, dtype))
+            if blk is None:
+                blk = self._blocks[(idx, dtype)] = native.Block(self.in_ch, self.out_ch, dtype, idx)
+            sd = self.state_dict(keep_vars=True)
+            sig = tuple((t.data_ptr(), t._version) for t in sd.values())
+            if self._packed_sig.get((idx, dtype)) != sig:
+                blk.load_weights(sd)
+                self._packed_sig[(idx, dtype)] = sig
+        x = x.detach()
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.to(torch.float32).contiguous()
+        n, _, h, w = x.shape
+        y = torch.empty((n, self.out_ch, h, w), device=x.device, dtype=torch.float32)
+        with torch.cuda.device(x.device):
+            blk.forward(x, y, torch.cuda.current_stream(x.device).cuda_stream)
+        return y
 
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)
         _bump_epoch()
         return out
+
+    def close(self):
+        for b in self._blocks.values():
+            b.close()
+        self._blocks.clear()
+        self._packed_sig.clear()
 
 
 class UNet(nn.Module):
@@ -89,20 +130,21 @@ class UNet(nn.Module):
             raise ValueError(f"compute_dtype must be one of {sorted(native.DTYPES)}")
         self.thresholds = tuple(float(t) for t in thresholds)
 
-        self.down1 = DoubleConv(n_channels, 64)
-        self.down2 = DoubleConv(64, 128)
-        self.down3 = DoubleConv(128, 256)
-        self.down4 = DoubleConv(256, 512)
+        cd = self.compute_dtype   # the blocks' own forward (called stand-alone) uses the model's precision plan
+        self.down1 = DoubleConv(n_channels, 64, cd)
+        self.down2 = DoubleConv(64, 128, cd)
+        self.down3 = DoubleConv(128, 256, cd)
+        self.down4 = DoubleConv(256, 512, cd)
         self.pool = nn.MaxPool2d(2)
-        self.bottleneck = DoubleConv(512, 1024)
+        self.bottleneck = DoubleConv(512, 1024, cd)
         self.up4 = nn.ConvTranspose2d(1024, 512, 2, stride=2)
-        self.conv4 = DoubleConv(1024, 512)
+        self.conv4 = DoubleConv(1024, 512, cd)
         self.up3 = nn.ConvTranspose2d(512, 256, 2, stride=2)
-        self.conv3 = DoubleConv(512, 256)
+        self.conv3 = DoubleConv(512, 256, cd)
         self.up2 = nn.ConvTranspose2d(256, 128, 2, stride=2)
-        self.conv2 = DoubleConv(256, 128)
+        self.conv2 = DoubleConv(256, 128, cd)
         self.up1 = nn.ConvTranspose2d(128, 64, 2, stride=2)
-        self.conv1 = DoubleConv(128, 64)
+        self.conv1 = DoubleConv(128, 64, cd)
         self.out_conv = nn.Conv2d(64, n_classes, kernel_size=1)
         nn.init.constant_(self.out_conv.bias, -4)  # unet_model.py:52-53
 
@@ -274,3 +316,6 @@ class UNet(nn.Module):
             h.close()
         self._handles.clear()
         self._packed_sig.clear()
+        for m in self.modules():
+            if isinstance(m, DoubleConv):
+                m.close()

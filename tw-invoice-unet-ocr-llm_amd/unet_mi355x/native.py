@@ -41,6 +41,33 @@ class TensorView(ctypes.Structure):
                 ("ndim", ctypes.c_int), ("shape", ctypes.c_int64 * 4)]
 
 
+class BlockConfig(ctypes.Structure):
+    _fields_ = [("in_ch", ctypes.c_int), ("out_ch", ctypes.c_int), ("dtype", ctypes.c_int), ("device", ctypes.c_int)]
+
+
+def tensor_views(state_dict):
+    """state_dict (name -> torch.Tensor / np.ndarray, any device) -> (TensorView array, arrays to keep alive):
+    floating tensors as contiguous host fp32 (numpy has no bfloat16: a model cast with .to(torch.bfloat16)
+    loads like the reference UNet does, its parameters simply read back in fp32), integers as int64."""
+    keep, views = [], []
+    for k, v in state_dict.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu()
+            arr = (v.to(torch.float32) if v.is_floating_point() else v).numpy()
+        else:
+            arr = np.asarray(v)
+        if arr.dtype.kind == "f":
+            arr = np.ascontiguousarray(arr, dtype=np.float32)
+            code = 0
+        else:
+            arr = np.ascontiguousarray(arr, dtype=np.int64)
+            code = 1
+        keep.append(arr)
+        shape = list(arr.shape) + [0] * (4 - arr.ndim)
+        views.append(TensorView(k.encode(), arr.ctypes.data, code, arr.ndim, (ctypes.c_int64 * 4)(*shape)))
+    return (TensorView * len(views))(*views), keep
+
+
 SIGNATURES = {
     "unet_create": (_i, [ctypes.POINTER(UnetConfig), ctypes.POINTER(_vp)]),
     "unet_load_weights": (_i, [_vp, ctypes.POINTER(TensorView), _i]),
@@ -66,6 +93,11 @@ SIGNATURES = {
     "unet_allgather": (_i, [_vp, _vp, _vp, _sz, _vp]),
     "unet_comm_destroy": (_i, [_vp]),
     "unet_destroy": (_i, [_vp]),
+    "unet_block_create": (_i, [ctypes.POINTER(BlockConfig), ctypes.POINTER(_vp)]),
+    "unet_block_load_weights": (_i, [_vp, ctypes.POINTER(TensorView), _i]),
+    "unet_block_reserve": (_i, [_vp, _i, _i, _i]),
+    "unet_block_forward": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp]),
+    "unet_block_destroy": (_i, [_vp]),
     "unet_last_error": (ctypes.c_char_p, []),
     "unet_abi_version": (_i, []),
     "unet_logit_cut": (ctypes.c_float, [ctypes.c_float]),
@@ -159,27 +191,9 @@ class Handle:
 
     def load_weights(self, state_dict) -> None:
         """state_dict: mapping name -> torch.Tensor / np.ndarray (any device); strict."""
-        keep, views = [], []
-        for k, v in state_dict.items():
-            if isinstance(v, torch.Tensor):
-                v = v.detach().cpu()
-                # numpy has no bfloat16: a model cast with .to(torch.bfloat16) loads like the
-                # reference UNet does (its parameters are simply read back in fp32)
-                arr = (v.to(torch.float32) if v.is_floating_point() else v).numpy()
-            else:
-                arr = np.asarray(v)
-            if arr.dtype.kind == "f":
-                arr = np.ascontiguousarray(arr, dtype=np.float32)
-                code = 0
-            else:
-                arr = np.ascontiguousarray(arr, dtype=np.int64)
-                code = 1
-            keep.append(arr)
-            shape = list(arr.shape) + [0] * (4 - arr.ndim)
-            views.append(TensorView(k.encode(), arr.ctypes.data, code, arr.ndim, (ctypes.c_int64 * 4)(*shape)))
-        arr_t = (TensorView * len(views))(*views)
+        arr_t, _keep = tensor_views(state_dict)
         with self.lock:
-            check(self.lib.unet_load_weights(self._h, arr_t, len(views)), "unet_load_weights")
+            check(self.lib.unet_load_weights(self._h, arr_t, len(arr_t)), "unet_load_weights")
 
     def workspace_bytes(self, n: int, h: int, w: int) -> int:
         return int(self.lib.unet_workspace_bytes(self._h, n, h, w))
@@ -350,6 +364,46 @@ class Handle:
         if getattr(self, "_h", None):
             self.lib.unet_destroy(self._h)
             self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Block:
+    """A stand-alone DoubleConv (unet_block_*): conv3x3 + BN + ReLU twice on the network's kernels."""
+
+    def __init__(self, in_ch: int, out_ch: int, dtype: str, device: int):
+        self.lib = load_library()
+        self.in_ch, self.out_ch, self.dtype, self.device = in_ch, out_ch, dtype, device
+        b = ctypes.c_void_p()
+        check(self.lib.unet_block_create(ctypes.byref(BlockConfig(in_ch, out_ch, DTYPES[dtype], device)), ctypes.byref(b)),
+              "unet_block_create")
+        self._b = b
+        self.lock = threading.Lock()
+
+    def load_weights(self, state_dict) -> None:
+        arr_t, _keep = tensor_views(state_dict)
+        with self.lock:
+            check(self.lib.unet_block_load_weights(self._b, arr_t, len(arr_t)), "unet_block_load_weights")
+
+    def forward(self, x: torch.Tensor, y: torch.Tensor, stream: int) -> None:
+        """x: device fp32 NCHW [N, in_ch, H, W] -> y: device fp32 NCHW [N, out_ch, H, W] (contiguous)."""
+        n, c, h, w = x.shape
+        if x.dtype != torch.float32 or not x.is_contiguous() or c != self.in_ch:
+            raise ValueError(f"x must be a contiguous float32 [N, {self.in_ch}, H, W] tensor")
+        if y.dtype != torch.float32 or not y.is_contiguous() or tuple(y.shape) != (n, self.out_ch, h, w):
+            raise ValueError(f"y must be a contiguous float32 {(n, self.out_ch, h, w)} tensor")
+        with self.lock:
+            check(self.lib.unet_block_reserve(self._b, n, h, w), "unet_block_reserve")
+            check(self.lib.unet_block_forward(self._b, x.data_ptr(), y.data_ptr(), n, h, w, stream), "unet_block_forward")
+
+    def close(self) -> None:
+        if getattr(self, "_b", None):
+            self.lib.unet_block_destroy(self._b)
+            self._b = None
 
     def __del__(self):
         try:
