@@ -1832,7 +1832,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
   if constexpr (HS != 0) {
     const TileXY t0 = tile_xy(0);
     issue_xs(0, t0);
-    if (items > 1) issue_xs(1, tile_xy(1));   // the loop DMAs each window two tiles ahead (below)
     wait_vm_barrier<0>();
     compute_halo(0, t0, C0{}, 0, C0{});
     compute_halo(0, t0, C0{}, 0, C1{});
@@ -1893,22 +1892,15 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     // stationary; the input window double-buffered, tile i in window i & 1).  A tile's 18 taps
     // run as two pipelined 9-tap phases (one per chunk) with ONE barrier each (instead of one per
     // 3-tap step):
-    //   1: chunk 1's halo computed from this tile's window | the nine taps of chunk 0
-    //      -> vmcnt + barrier (the next tile's window landed; chunk 1's halo visible; every read of
-    //      halo buffer 0 and of this tile's window done)
-    //   2: the window of the tile after next DMA'd into this tile's window buffer | the next tile's
-    //      chunk-0 halo computed into buffer 0 | the nine taps of chunk 1
+    //   1: the next tile's window DMA'd | chunk 1's halo computed from this tile's window | the
+    //      nine taps of chunk 0  -> vmcnt(0) + barrier (window landed; chunk 1's halo visible;
+    //      every read of halo buffer 0 done)
+    //   2: the next tile's chunk-0 halo computed into buffer 0 | the nine taps of chunk 1
     //      -> barrier (visible to the next tile's phase 1; every read of buffer 1 done)
-    // A window is DMA'd two phases before its first read (round 5; it was DMA'd in phase 1 of the
-    // tile before, after the epilogue stores of that tile's predecessor), so the phase-1 wait leaves
-    // the previous tile's epilogue stores -- 80 KB per block, issued after the window DMA -- in flight:
-    // vmcnt(kEpiStores) instead of a drain of every store.  Each wave computes its share of a halo
-    // after the phase's MFMAs (profiles/tune_r2j_fused_phases.txt: computing it before them on waves
-    // 0-3, so that the two waves of a SIMD overlap halo work with MFMAs, and three 6-tap phases per
-    // tile instead of two, were no faster).
-    // Vector-memory stores of one tile's EPI_POOL epilogue per wave when every lane of the tile is
-    // inside the image: TP pixel groups x (2 skip + 2 pooled 16-byte stores) (checked in the ISA).
-    constexpr int kEpiStores = 4 * TP;
+    // A window buffer is re-filled one tile after its last read (two barriers later).  Each wave
+    // computes its share of a halo after the phase's MFMAs (profiles/tune_r2j_fused_phases.txt:
+    // computing it before them on waves 0-3, so that the two waves of a SIMD overlap halo work
+    // with MFMAs, and three 6-tap phases per tile instead of two, were no faster).
     auto taps9 = [&](int ch) {   // the nine taps of chunk ch (halo buffer ch, weight steps 3ch .. 3ch+2)
       const char* hs9[9];
       const char* ws9[9];
@@ -1926,15 +1918,13 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       compute_halo(i, tc, cbc, decltype(cbc)::value, C1{});
     };
     TileXY cur = tile_xy(0);
-    bool prev_full = false;   // the previous tile's epilogue issued all kEpiStores stores on every wave
     for (int item = 0; item < items; ++item) {
       const bool more = item + 1 < items;
       const TileXY nxt = more ? tile_xy(item + 1) : cur;
+      if (more) issue_xs(item + 1, nxt);
       taps9(0);
       halo_all(item, cur, C1{});
-      if (prev_full) wait_vm_barrier<kEpiStores>();   // window item + 1 landed (issued before those stores)
-      else wait_vm_barrier<0>();
-      if (item + 2 < items) issue_xs(item + 2, tile_xy(item + 2));   // into buffer item & 1: last read in phase 1
+      wait_vm_barrier<0>();
       taps9(1);
       if (more) halo_all(item + 1, nxt, C0{});
       wait_vm_barrier<63>();   // barrier only: no load is waited for here
@@ -1943,7 +1933,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
         conv_epilogue<TO, TQ, TP, EPI, TW, 0, 1>(a, *reinterpret_cast<const f32x4(*)[4][TP]>(&acc[4 * h]), cur.n,
                                                  cur.ty * 16, cur.tx * TW, wp * TP, ct * BR + 64 * h, bias_s + 64 * h,
                                                  headw_s, headb_s);
-      prev_full = cur.ty * 16 + 16 <= H && cur.tx * TW + TW <= W;
       init_acc_bias(0, TC);
       cur = nxt;
     }
