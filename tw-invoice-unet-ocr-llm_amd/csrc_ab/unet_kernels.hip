@@ -1517,8 +1517,7 @@ __device__ __forceinline__ void wait_vm_barrier_rt(int n) {
 // the barriers, 2 = no MFMAs, 3 = no LDS fragment reads, 4 = no LDS-DMA in the loop (the slots keep
 // the prologue's bytes); 5 = no tile epilogue (the accumulators are kept
 // alive, nothing is stored) -- the per-tile epilogue's share of a layer, wrong outputs by construction;
-// 6 = the epilogue's arithmetic without its stores; 7 = its stores (zeros) without the arithmetic;
-// 8 = every 32-channel chunk's halo from the first 64 bytes of its 128-byte line (issue_halo).
+// 6 = the epilogue's arithmetic without its stores; 7 = its stores (zeros) without the arithmetic.
 template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a) {
   using G = Ring8Geom<T, TCW, NS, TPS, WST, HS>;
@@ -1656,11 +1655,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
       }
     }
     const uint32_t dst = lds0 + (hq_seq & 1) * HALO_BYTES + wave * HI * 1024;
-    // (ablation 8, timing only: every chunk of a 128-byte line loads the line's first 64 bytes, so each
-    // line of the halo is fetched once -- wrong values, the cost of the sibling-chunk re-fetch)
-    const int hoff = ABL == 8 ? (hq_c & ~1) * 64 : hq_c * 64;
 #pragma unroll
-    for (int j = 0; j < HI; ++j) glds16_s(hsrc[j] + hoff, dst + j * 1024);
+    for (int j = 0; j < HI; ++j) glds16_s(hsrc[j] + hq_c * 64, dst + j * 1024);
     ++hq_seq;
     if (++hq_c == nch) { hq_c = 0; ++hq_i; }
   };
@@ -2551,9 +2547,8 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
       case CFG_RING_FUSED_IN:
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ, ABL>(a, s);
         break;
-      case CFG_RING8_R128:   // (8: the halo-line ablation, issue_halo)
-        if constexpr (ABL >= 1 && ABL <= 8 && EPI != EPI_HEAD && sizeof(T) == 2)
-          return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ, 0, ABL>(a, s);
+      case CFG_RING8_R128:
+        if constexpr (ABL >= 1 && ABL <= 7 && EPI != EPI_HEAD) return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ, 0, ABL>(a, s);
         break;
       case CFG_RING8_R64_T9:
         if constexpr (ABL >= 5 && ABL <= 7 && EPI != EPI_HEAD) return launch_ring8<T, 4, 2, EPI, 9, 0, TO, TQ, 0, ABL>(a, s);

@@ -1,0 +1,210 @@
+// GPU preprocessing: the resize + convert("RGB") + /255 + CHW of
+// inference.py:30-44 and :62-64, bit-exact with Pillow's Image.resize default filter.
+//
+// Pillow resizes 8-bit images with a separable two-pass fixed-point resampler (horizontal pass
+// into an 8-bit intermediate over the rows the vertical pass needs, then the vertical pass):
+// per output sample  clip8((1 << 21) + sum_k in[k] * coeff[k]) with 22 fractional bits, the
+// coefficients being the normalised bicubic (a = -0.5) weights over a support widened by the
+// downscale factor (antialiasing), rounded half away from zero.  The coefficient tables are
+// computed on the host in double precision with the same operation order (unet_capi.cpp,
+// resample_coeffs) and the kernels here do the integer arithmetic, so every output byte equals
+// Pillow's.  The oracle (oracle/pil_resample.py) restates the same algorithm in numpy and is
+// itself checked against Pillow (tests/test_preprocess_cpu.py).
+#include "unet_internal.h"
+
+#include <algorithm>
+
+namespace unet {
+
+namespace {
+constexpr int kResamplePrec = 22;   // Pillow PRECISION_BITS = 32 - 8 - 2
+
+__device__ __forceinline__ int clip8_fixed(int v) {
+  const int s = v >> kResamplePrec;   // arithmetic shift, as Pillow's clip8 lookup
+  return s < 0 ? 0 : (s > 255 ? 255 : s);
+}
+}  // namespace
+
+// The tap loops below take the taps eight at a time with all of a group's coefficient and pixel
+// loads issued before the first multiply (the loads are independent; a loop of one tap per
+// iteration waits out a memory latency per tap, 18 us per pass on a 600x400 photo), and the
+// channel count is a template argument so the accumulators stay in registers.  Integer sums are
+// exact, so the grouping does not change a byte.
+constexpr int kTapGroup = 8;
+
+// Horizontal pass: tmp[r][xx][c] = clip8(sum_x src[y0 + r][xmin(xx) + x][c] * kh[xx][x]).
+// One thread per (row, output column), all channels.
+template <int C>
+__global__ __launch_bounds__(256) void resample_h_kernel(const uint8_t* __restrict__ src, int src_stride, int y0,
+                                                        int rows, const int* __restrict__ bounds,
+                                                        const int* __restrict__ kk, int ksize, int ow,
+                                                        uint8_t* __restrict__ tmp) {
+  const int xx = blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.y;
+  if (xx >= ow || r >= rows) return;
+  const int xmin = bounds[2 * xx], n = bounds[2 * xx + 1];
+  const int* k = kk + (size_t)xx * ksize;
+  const uint8_t* row = src + (size_t)(y0 + r) * src_stride + (size_t)xmin * C;
+  int acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 1 << (kResamplePrec - 1);
+  for (int x0 = 0; x0 < n; x0 += kTapGroup) {
+    int w[kTapGroup], px[kTapGroup][C];
+#pragma unroll
+    for (int j = 0; j < kTapGroup; ++j) {
+      const int t = min(x0 + j, n - 1);   // past the last tap: a valid address, weight 0
+      const int wt = k[t];
+      w[j] = x0 + j < n ? wt : 0;
+#pragma unroll
+      for (int c = 0; c < C; ++c) px[j][c] = (int)row[t * C + c];
+    }
+#pragma unroll
+    for (int j = 0; j < kTapGroup; ++j)
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] += px[j][c] * w[j];
+  }
+  uint8_t* dst = tmp + ((size_t)r * ow + xx) * C;
+#pragma unroll
+  for (int c = 0; c < C; ++c) dst[c] = (uint8_t)clip8_fixed(acc[c]);
+}
+
+// Vertical pass fused with the final conversion: out[c][yy][xx] = clip8(...) / 255 (fp32, the
+// reference's np.float32 division), gray (C = 1) replicated to 3 planes as convert("RGB").
+template <int C>
+__global__ __launch_bounds__(256) void resample_v_kernel(const uint8_t* __restrict__ src, int src_stride,
+                                                        const int* __restrict__ bounds, const int* __restrict__ kk,
+                                                        int ksize, int oh, int ow, float* __restrict__ out) {
+  const int xx = blockIdx.x * 256 + threadIdx.x;
+  const int yy = blockIdx.y;
+  if (xx >= ow || yy >= oh) return;
+  const int ymin = bounds[2 * yy], n = bounds[2 * yy + 1];
+  const int* k = kk + (size_t)yy * ksize;
+  const uint8_t* col = src + (size_t)ymin * src_stride + (size_t)xx * C;
+  int acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 1 << (kResamplePrec - 1);
+  for (int y0 = 0; y0 < n; y0 += kTapGroup) {
+    int w[kTapGroup], px[kTapGroup][C];
+#pragma unroll
+    for (int j = 0; j < kTapGroup; ++j) {
+      const int t = min(y0 + j, n - 1);
+      const int wt = k[t];
+      w[j] = y0 + j < n ? wt : 0;
+#pragma unroll
+      for (int c = 0; c < C; ++c) px[j][c] = (int)col[(size_t)t * src_stride + c];
+    }
+#pragma unroll
+    for (int j = 0; j < kTapGroup; ++j)
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] += px[j][c] * w[j];
+  }
+  const size_t plane = (size_t)oh * ow, o = (size_t)yy * ow + xx;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) out[c * plane + o] = (float)clip8_fixed(acc[C == 3 ? c : 0]) / 255.0f;
+}
+
+// No vertical resampling (ih == oh): convert the (horizontally resampled or original) rows.
+__global__ __launch_bounds__(256) void to_planar_f32_kernel(const uint8_t* __restrict__ src, int src_stride, int C,
+                                                           int oh, int ow, float* __restrict__ out) {
+  const int xx = blockIdx.x * 256 + threadIdx.x;
+  const int yy = blockIdx.y;
+  if (xx >= ow || yy >= oh) return;
+  const uint8_t* p = src + (size_t)yy * src_stride + (size_t)xx * C;
+  const size_t plane = (size_t)oh * ow, o = (size_t)yy * ow + xx;
+  for (int c = 0; c < 3; ++c) out[c * plane + o] = (float)p[C == 3 ? c : 0] / 255.0f;
+}
+
+hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int C, uint8_t* tmp, float* out,
+                           hipStream_t s) {
+  if ((C != 1 && C != 3) || p.oh <= 0 || p.ow <= 0) return hipErrorInvalidValue;
+  const uint8_t* src = img;
+  int stride = p.iw * C;
+  if (p.need_h) {
+    const dim3 grid((unsigned)((p.ow + 255) / 256), (unsigned)p.h_rows);
+    if (C == 3)
+      hipLaunchKernelGGL(resample_h_kernel<3>, grid, dim3(256), 0, s, img, p.iw * C, p.h_y0, p.h_rows, p.h_bounds,
+                         p.h_kk, p.h_ksize, p.ow, tmp);
+    else
+      hipLaunchKernelGGL(resample_h_kernel<1>, grid, dim3(256), 0, s, img, p.iw * C, p.h_y0, p.h_rows, p.h_bounds,
+                         p.h_kk, p.h_ksize, p.ow, tmp);
+    src = tmp;
+    stride = p.ow * C;
+  }
+  const dim3 grid((unsigned)((p.ow + 255) / 256), (unsigned)p.oh);
+  if (p.need_v && C == 3)
+    hipLaunchKernelGGL(resample_v_kernel<3>, grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize, p.oh,
+                       p.ow, out);
+  else if (p.need_v)
+    hipLaunchKernelGGL(resample_v_kernel<1>, grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize, p.oh,
+                       p.ow, out);
+  else
+    hipLaunchKernelGGL(to_planar_f32_kernel, grid, dim3(256), 0, s, src, stride, C, p.oh, p.ow, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// Crop statistics (inference.py:92-127) on the device photo: per (image, field) mask box, the
+// crop rectangle in photo pixels and the sum of the crop's uint8 values, so the host applies the
+// reference's rejection rules without reading pixels.  The rectangle arithmetic is the
+// reference's, in float64 as Python evaluates it: scale = ow / IMG_SIZE (true division),
+// x1 = int(mx1 * scale) (truncation), pad = int((x2 - x1) * 0.15), clamp to [0, ow] / [0, oh].
+// "arr.mean() < 3" over the crop's uint8 values (numpy's float64 pairwise sum of integers is
+// exact below 2^53) is "sum < 3 * count" -- the host tests that.  Grid (row blocks, boxes); each
+// block sums its rows (64-bit, one atomic per wave) into sums[box], zeroed by the launcher.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void crop_rect(const int* b, int ih, int iw, int bh, int bw, double pad, int& x1, int& y1,
+                                          int& x2, int& y2) {
+  const double sx = (double)iw / (double)bw, sy = (double)ih / (double)bh;
+  x1 = (int)((double)b[0] * sx);
+  x2 = (int)((double)b[2] * sx);
+  y1 = (int)((double)b[1] * sy);
+  y2 = (int)((double)b[3] * sy);
+  const int px = (int)((double)(x2 - x1) * pad), py = (int)((double)(y2 - y1) * pad);
+  x1 = max(0, x1 - px);
+  y1 = max(0, y1 - py);
+  x2 = min(iw, x2 + px);
+  y2 = min(ih, y2 + py);
+}
+
+__global__ __launch_bounds__(256) void crop_stats_kernel(const uint8_t* __restrict__ img, int ih, int iw, int C,
+                                                        const int* __restrict__ boxes, int bh, int bw, double pad,
+                                                        int* __restrict__ rects,
+                                                        unsigned long long* __restrict__ sums) {
+  const int i = blockIdx.y;
+  const int* b = boxes + 4 * i;
+  if (b[2] < 0) {   // empty mask
+    if (blockIdx.x == 0 && threadIdx.x < 4) rects[4 * i + threadIdx.x] = -1;
+    return;
+  }
+  int x1, y1, x2, y2;
+  crop_rect(b, ih, iw, bh, bw, pad, x1, y1, x2, y2);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    rects[4 * i] = x1;
+    rects[4 * i + 1] = y1;
+    rects[4 * i + 2] = x2;
+    rects[4 * i + 3] = y2;
+  }
+  if (x2 <= x1 || y2 <= y1) return;
+  const int rowlen = (x2 - x1) * C;
+  unsigned long long acc = 0;
+  for (int y = y1 + (int)blockIdx.x; y < y2; y += (int)gridDim.x) {
+    const uint8_t* row = img + ((size_t)y * iw + x1) * C;
+    for (int k = threadIdx.x; k < rowlen; k += 256) acc += row[k];
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(sums + i, acc);
+}
+
+hipError_t launch_crop_stats(const uint8_t* img, int ih, int iw, int C, const int* boxes, int n_boxes, int bh, int bw,
+                             double pad, int* rects, unsigned long long* sums, hipStream_t s) {
+  if ((C != 1 && C != 3) || ih <= 0 || iw <= 0 || bh <= 0 || bw <= 0 || n_boxes <= 0) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(sums, 0, (size_t)n_boxes * sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  const int rows_per = 8;
+  const unsigned gx = (unsigned)std::min(64, (ih + rows_per - 1) / rows_per);
+  hipLaunchKernelGGL(crop_stats_kernel, dim3(gx, (unsigned)n_boxes), dim3(256), 0, s, img, ih, iw, C, boxes, bh, bw,
+                     pad, rects, sums);
+  return hipGetLastError();
+}
+
+}  // namespace unet
