@@ -3,7 +3,8 @@
 Times the drop-in run_unet (inference.py:50-129 restated in unet_mi355x/inference.py) on a
 600x400 RGB photo at the fp32 default and the mixed plan: the end-to-end median, a cProfile of
 the host side, and each stage of the call on its own (host wall time with a synchronisation
-after the stage, and the device time of the stage between HIP events).
+after the stage, and the device time of the stage between HIP events) -- the photo graph that
+run_unet launches (round 5) and, for reference, its pieces as separate calls.
 Usage: python tools/prof_run_unet.py [--calls 50]
 """
 import argparse
@@ -67,11 +68,16 @@ def main():
             model = inf._cached_model(ck, dtype)
             st = inf._staging[str(inf.DEVICE)]
             stream = torch.cuda.current_stream(dev)
-            arr = np.asarray(pil)
+            arr = inf.photo_array(pil)
             img = st.upload(arr)
+            graph = st.photo_graph(model, img)
             stages = {
                 "cached_model": lambda: inf._cached_model(ck, dtype),
-                "asarray": lambda: np.asarray(pil),
+                "photo_array": lambda: inf.photo_array(pil),
+                "stage_pinned": lambda: st.stage(arr),
+                # the whole device part of the call as run_unet launches it: upload, resize, forward, boxes,
+                # crop statistics and the four copies back, one graph
+                "photo_graph": lambda: graph.launch(stream.cuda_stream),
                 "upload": lambda: st.upload(arr),
                 "preprocess": lambda: model.preprocess(img, inf.IMG_SIZE, out=st.x[0]),
                 "forward_boxes": lambda: model.forward_boxes(st.x, masks="u8", out=(st.m, st.b)),

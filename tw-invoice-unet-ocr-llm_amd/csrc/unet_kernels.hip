@@ -61,7 +61,7 @@ int ring_tps(int cfg) {
 }
 int cfg_limit() {
 #ifdef UNET_ABLATION
-  return CFG_COUNT + 16 * 8;
+  return CFG_COUNT + 16 * 10;
 #else
   return CFG_RING_R64_W12;   // the configurations after it are ablation-build only
 #endif
@@ -1518,7 +1518,8 @@ __device__ __forceinline__ void wait_vm_barrier_rt(int n) {
 // the prologue's bytes); 5 = no tile epilogue (the accumulators are kept
 // alive, nothing is stored) -- the per-tile epilogue's share of a layer, wrong outputs by construction;
 // 6 = the epilogue's arithmetic without its stores; 7 = its stores (zeros) without the arithmetic;
-// 8 = every 32-channel chunk's halo from the first 64 bytes of its 128-byte line (issue_halo).
+// 8 = every 32-channel chunk's halo from the first 64 bytes of its 128-byte line (issue_halo); 9 = no
+// halo DMA for odd chunks (issue_halo).
 template <typename T, int TCW, int NS, int EPI, int TPS, int WST, typename TO, typename TQ, int HS = 0, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a) {
   using G = Ring8Geom<T, TCW, NS, TPS, WST, HS>;
@@ -1658,9 +1659,13 @@ __global__ __launch_bounds__(512, 2) void conv3x3_ring8_kernel(const IgemmArgs a
     const uint32_t dst = lds0 + (hq_seq & 1) * HALO_BYTES + wave * HI * 1024;
     // (ablation 8, timing only: every chunk of a 128-byte line loads the line's first 64 bytes, so each
     // line of the halo is fetched once -- wrong values, the cost of the sibling-chunk re-fetch)
+    // (ablation 9: odd chunks issue no halo DMA at all -- their taps read the stale buffer; the counted
+    // waits then wait for younger loads only, which is safe: timing only)
     const int hoff = ABL == 8 ? (hq_c & ~1) * 64 : hq_c * 64;
+    if (ABL != 9 || (hq_c & 1) == 0) {
 #pragma unroll
-    for (int j = 0; j < HI; ++j) glds16_s(hsrc[j] + hoff, dst + j * 1024);
+      for (int j = 0; j < HI; ++j) glds16_s(hsrc[j] + hoff, dst + j * 1024);
+    }
     ++hq_seq;
     if (++hq_c == nch) { hq_c = 0; ++hq_i; }
   };
@@ -2552,7 +2557,7 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
         if constexpr (sizeof(T) == 2 && EPI == EPI_POOL) return launch_ring<T, 1, 4, 4, 3, EPI, 3, 1, TO, TQ, ABL>(a, s);
         break;
       case CFG_RING8_R128:   // (8: the halo-line ablation, issue_halo)
-        if constexpr (ABL >= 1 && ABL <= 8 && EPI != EPI_HEAD && sizeof(T) == 2)
+        if constexpr (ABL >= 1 && ABL <= 9 && EPI != EPI_HEAD && sizeof(T) == 2)
           return launch_ring8<T, 8, 3, EPI, 3, 0, TO, TQ, 0, ABL>(a, s);
         break;
       case CFG_RING8_R64_T9:
@@ -2629,7 +2634,7 @@ static hipError_t launch_typed(int cfg, int taps, int epi, const IgemmArgs& a, h
     }
     switch (cfg / 16) {
       UNET_ABL_CASE(1) UNET_ABL_CASE(2) UNET_ABL_CASE(3) UNET_ABL_CASE(4) UNET_ABL_CASE(5) UNET_ABL_CASE(6)
-      UNET_ABL_CASE(7) UNET_ABL_CASE(8)
+      UNET_ABL_CASE(7) UNET_ABL_CASE(8) UNET_ABL_CASE(9)
       default: return hipErrorInvalidValue;
     }
 #undef UNET_ABL_CASE
