@@ -131,7 +131,8 @@ int unet_forward_boxes(unet_handle* h, const void* x, int x_layout, int x_dtype,
 /* GPU preprocessing of one photo (inference.py:62-64 + preprocess, :30-44):
  * PIL Image.resize((ow, oh)) with Pillow's default BICUBIC filter -- bit-exact with Pillow's
  * fixed-point separable resampler --, convert("RGB") (gray replicated), /255 as float32, CHW.
- * img: device uint8 HWC [ih][iw][channels], channels 3 (mode "RGB") or 1 (mode "L");
+ * img: device uint8 HWC [ih][iw][channels], channels 3 (mode "RGB"), 1 (mode "L") or 4 (RGBX: Pillow's own
+ *      in-memory layout of an "RGB" image, 4 bytes per pixel, the 4th ignored -- uploaded without repacking);
  * x:   device fp32 [3][oh][ow] (e.g. one image's slot of the unet_forward input batch).
  * Coefficient tables are cached per (ih, iw, oh, ow) in the handle (first call per geometry
  * uploads them synchronously).  Stream-ordered on hip_stream. */
@@ -147,7 +148,8 @@ int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channel
  * np.array(crop).mean() < 3  <=>  sum < 3 * (x2 - x1) * (y2 - y1) * channels (numpy's float64 sum
  * of the integers is exact).  img: device uint8 HWC [ih][iw][channels] (unet_preprocess's input);
  * boxes: device int32 [n_boxes][4]; rects: device int32 [n_boxes][4] (x1, y1, x2, y2; -1s for an
- * empty box); sums: device uint64 [n_boxes].  Needs no handle; stream-ordered on hip_stream. */
+ * empty box); sums: device uint64 [n_boxes] (channels 4 = RGBX: the sum over R, G, B).  Needs no handle;
+ * stream-ordered on hip_stream. */
 int unet_crop_stats(const void* img, int ih, int iw, int channels, const int32_t* boxes, int n_boxes,
                     int box_h, int box_w, double pad, int32_t* rects, uint64_t* sums, void* hip_stream);
 

@@ -825,10 +825,12 @@ def test_reference_pages_in_bs32_fp32_batch_and_batch_invariance(monkeypatch):
                                    (512, 900, 3), (512, 512, 3), (390, 517, 1), (37, 23, 3), (3024, 4032, 3)])
 def test_preprocess_bit_exact_with_pillow(h, w, c):
     """unet_preprocess (GPU) == PIL Image.resize((512, 512)) (default BICUBIC) + convert("RGB")
-    + /255, bit for bit: down / up / one-axis / identity geometries, RGB and L, a 12 MP photo."""
+    + /255, bit for bit: down / up / one-axis / identity geometries, RGB and L, a 12 MP photo; and the
+    same RGB photos uploaded as RGBX (Pillow's in-memory layout, run_unet's upload) with a random 4th
+    byte, which must be ignored."""
     from PIL import Image
     rng = np.random.default_rng(h + 3 * w)
-    arr = rng.integers(0, 256, (h, w, c) if c == 3 else (h, w), dtype=np.uint8)
+    arr = rng.integers(0, 256, (h, w, 3) if c == 3 else (h, w), dtype=np.uint8)
     if h == 3024:   # smooth photo-like content (strong low-pass response, clip8 at both ends)
         yy, xx = np.mgrid[0:h, 0:w]
         arr = (127.5 + 127.5 * (np.sin(yy / 37.0) * np.cos(xx / 53.0))[..., None] + rng.normal(0, 20, (h, w, 3))
@@ -839,6 +841,10 @@ def test_preprocess_bit_exact_with_pillow(h, w, c):
     got = m.preprocess(torch.from_numpy(arr).to(DEV)).cpu().numpy()[0]
     assert got.shape == (3, 512, 512)
     assert np.array_equal(got, ref.transpose(2, 0, 1))
+    if c == 3:
+        rgbx = np.concatenate([arr, rng.integers(0, 256, (h, w, 1), dtype=np.uint8)], -1)
+        got4 = m.preprocess(torch.from_numpy(rgbx).to(DEV)).cpu().numpy()[0]
+        assert np.array_equal(got4, got)
     if h < 2000:   # the numpy restatement agrees too (checker of the checker)
         from oracle import pil_resample as pr
         assert np.array_equal(got, pr.to_input(arr))
@@ -925,6 +931,11 @@ def test_crop_stats_match_host_crop_rules(h, w, c):
         sums = torch.empty((len(boxes),), dtype=torch.int64, device=DEV)
         img = torch.from_numpy(arr.reshape(h, w, c)).to(DEV)
         native.crop_stats(img, b, 512, 512, inf.CROP_PAD, rects, sums, torch.cuda.current_stream().cuda_stream)
+        if c == 3:   # the RGBX upload: the same rectangles and sums over R, G, B (the 4th byte ignored)
+            img4 = torch.from_numpy(np.concatenate([arr, rng.integers(0, 256, (h, w, 1), dtype=np.uint8)], -1)).to(DEV)
+            r4, s4 = torch.empty_like(rects), torch.empty_like(sums)
+            native.crop_stats(img4, b, 512, 512, inf.CROP_PAD, r4, s4, torch.cuda.current_stream().cuda_stream)
+            assert torch.equal(r4, rects) and torch.equal(s4, sums)
         rects, sums = rects.cpu().numpy(), sums.cpu().numpy()
         for i, box in enumerate(boxes):
             if box[2] < 0:

@@ -151,3 +151,36 @@ def test_doubleconv_standalone_surface_on_cpu():
     for cin, cout in ((5, 64), (3, 128), (64, 96)):
         rc = lib.unet_block_create(ctypes.byref(native.BlockConfig(cin, cout, 1, 0)), ctypes.byref(b))
         assert rc == native.UNET_ESHAPE and b"DoubleConv" in lib.unet_last_error(), (cin, cout)
+
+
+def test_copy_rgbx_equals_the_photo_pixels():
+    """run_unet's upload of an "RGB" photo (inference.copy_rgbx): Pillow's own RGBX pixels through its
+    zero-copy Arrow export, whose R, G, B bytes equal np.asarray(photo) -- plain, odd-sized, 1 x 1, cropped
+    and converted photos; None (the caller packs with photo_array) for other modes, a too small buffer and
+    a photo Pillow keeps in several memory blocks."""
+    from PIL import Image
+    from unet_mi355x import inference as inf
+    rng = np.random.default_rng(3)
+    base = Image.fromarray(rng.integers(0, 256, (400, 600, 3), dtype=np.uint8))
+    photos = [base, Image.fromarray(rng.integers(0, 256, (23, 37, 3), dtype=np.uint8)),
+              Image.fromarray(rng.integers(0, 256, (1, 1, 3), dtype=np.uint8)), base.crop((13, 7, 301, 222)),
+              Image.fromarray(rng.integers(0, 256, (50, 70, 4), dtype=np.uint8), "RGBA").convert("RGB"),
+              base.convert("L").convert("RGB")]
+    for p in photos:
+        w, h = p.size
+        buf = np.full(w * h * 4 + 64, 7, np.uint8)
+        shape = inf.copy_rgbx(p, buf.ctypes.data, buf.size)
+        if shape is None:   # the export is an optimisation: an older Pillow may not have it
+            continue
+        assert shape == (h, w, 4)
+        px = buf[:w * h * 4].reshape(h, w, 4)
+        assert np.array_equal(px[..., :3], np.asarray(p)), p.size
+        assert (buf[w * h * 4:] == 7).all()
+    small = np.empty(16, np.uint8)
+    assert inf.copy_rgbx(base, small.ctypes.data, small.size) is None
+    assert inf.copy_rgbx(base.convert("L"), small.ctypes.data, 1 << 30) is None
+    assert inf.copy_rgbx(base.convert("RGBA"), small.ctypes.data, 1 << 30) is None
+    big = Image.new("RGB", (4032, 3024))
+    huge = np.empty(4032 * 3024 * 4, np.uint8)
+    shape = inf.copy_rgbx(big, huge.ctypes.data, huge.size)
+    assert shape is None or shape == (3024, 4032, 4)

@@ -1211,7 +1211,8 @@ int unet_forward_boxes(unet_handle* h, const void* x, int x_layout, int x_dtype,
 int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channels, float* x, int oh, int ow,
                     void* stream) {
   if (!h || !img || !x) return fail(UNET_EINVAL, "null argument");
-  if (channels != 1 && channels != 3) return fail(UNET_EINVAL, "channels must be 1 (L) or 3 (RGB)");
+  if (channels != 1 && channels != 3 && channels != 4)
+    return fail(UNET_EINVAL, "channels must be 1 (L), 3 (RGB) or 4 (RGBX: Pillow's in-memory RGB, the 4th byte ignored)");
   if (ih <= 0 || iw <= 0 || oh <= 0 || ow <= 0 || (long long)ih * iw > (1LL << 30) || oh > 16384 || ow > 16384)
     return fail(UNET_EINVAL, "bad image or output size");
   DeviceGuard g(h->cfg.device);
@@ -1256,7 +1257,8 @@ int unet_preprocess(unet_handle* h, const void* img, int ih, int iw, int channel
 int unet_crop_stats(const void* img, int ih, int iw, int channels, const int32_t* boxes, int n_boxes, int box_h,
                     int box_w, double pad, int32_t* rects, uint64_t* sums, void* stream) {
   if (!img || !boxes || !rects || !sums) return fail(UNET_EINVAL, "null argument");
-  if (channels != 1 && channels != 3) return fail(UNET_EINVAL, "channels must be 1 (L) or 3 (RGB)");
+  if (channels != 1 && channels != 3 && channels != 4)
+    return fail(UNET_EINVAL, "channels must be 1 (L), 3 (RGB) or 4 (RGBX: Pillow's in-memory RGB, the 4th byte ignored)");
   if (ih <= 0 || iw <= 0 || (long long)ih * iw > (1LL << 30) || box_h <= 0 || box_w <= 0 || n_boxes <= 0 ||
       n_boxes > 65535 || !(pad >= 0.0 && pad < 1.0))
     return fail(UNET_EINVAL, "bad image size, box geometry, box count or pad");
@@ -1377,7 +1379,8 @@ int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih
                             uint64_t* sums, void* h_masks, void* h_boxes, void* h_rects, void* h_sums,
                             unet_graph** out) {
   if (!h || !img || !x || !boxes || !rects || !sums || !out) return fail(UNET_EINVAL, "null argument");
-  if (channels != 1 && channels != 3) return fail(UNET_EINVAL, "channels must be 1 (L) or 3 (RGB)");
+  if (channels != 1 && channels != 3 && channels != 4)
+    return fail(UNET_EINVAL, "channels must be 1 (L), 3 (RGB) or 4 (RGBX: Pillow's in-memory RGB, the 4th byte ignored)");
   if (ih <= 0 || iw <= 0 || (long long)ih * iw > (1LL << 30) || size <= 0 || size > 16384)
     return fail(UNET_EINVAL, "bad image or network size");
   if (!(pad >= 0.0 && pad < 1.0)) return fail(UNET_EINVAL, "bad pad");

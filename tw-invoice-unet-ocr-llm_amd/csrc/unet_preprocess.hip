@@ -32,9 +32,11 @@ __device__ __forceinline__ int clip8_fixed(int v) {
 // exact, so the grouping does not change a byte.
 constexpr int kTapGroup = 8;
 
-// Horizontal pass: tmp[r][xx][c] = clip8(sum_x src[y0 + r][xmin(xx) + x][c] * kh[xx][x]).
-// One thread per (row, output column), all channels.
-template <int C>
+// Source pixels: C channels of S bytes per pixel -- RGB (3, 3), L (1, 1), or Pillow's own in-memory
+// RGB layout RGBX (3, 4: the fourth byte is padding, never read), which the drop-in uploads as is.
+// Horizontal pass: tmp[r][xx][c] = clip8(sum_x src[y0 + r][xmin(xx) + x][c] * kh[xx][x]) (C bytes per
+// pixel).  One thread per (row, output column), all channels.
+template <int C, int S>
 __global__ __launch_bounds__(256) void resample_h_kernel(const uint8_t* __restrict__ src, int src_stride, int y0,
                                                         int rows, const int* __restrict__ bounds,
                                                         const int* __restrict__ kk, int ksize, int ow,
@@ -44,7 +46,7 @@ __global__ __launch_bounds__(256) void resample_h_kernel(const uint8_t* __restri
   if (xx >= ow || r >= rows) return;
   const int xmin = bounds[2 * xx], n = bounds[2 * xx + 1];
   const int* k = kk + (size_t)xx * ksize;
-  const uint8_t* row = src + (size_t)(y0 + r) * src_stride + (size_t)xmin * C;
+  const uint8_t* row = src + (size_t)(y0 + r) * src_stride + (size_t)xmin * S;
   int acc[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) acc[c] = 1 << (kResamplePrec - 1);
@@ -56,7 +58,7 @@ __global__ __launch_bounds__(256) void resample_h_kernel(const uint8_t* __restri
       const int wt = k[t];
       w[j] = x0 + j < n ? wt : 0;
 #pragma unroll
-      for (int c = 0; c < C; ++c) px[j][c] = (int)row[t * C + c];
+      for (int c = 0; c < C; ++c) px[j][c] = (int)row[t * S + c];
     }
 #pragma unroll
     for (int j = 0; j < kTapGroup; ++j)
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(256) void resample_h_kernel(const uint8_t* __restri
 
 // Vertical pass fused with the final conversion: out[c][yy][xx] = clip8(...) / 255 (fp32, the
 // reference's np.float32 division), gray (C = 1) replicated to 3 planes as convert("RGB").
-template <int C>
+template <int C, int S>
 __global__ __launch_bounds__(256) void resample_v_kernel(const uint8_t* __restrict__ src, int src_stride,
                                                         const int* __restrict__ bounds, const int* __restrict__ kk,
                                                         int ksize, int oh, int ow, float* __restrict__ out) {
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(256) void resample_v_kernel(const uint8_t* __restri
   if (xx >= ow || yy >= oh) return;
   const int ymin = bounds[2 * yy], n = bounds[2 * yy + 1];
   const int* k = kk + (size_t)yy * ksize;
-  const uint8_t* col = src + (size_t)ymin * src_stride + (size_t)xx * C;
+  const uint8_t* col = src + (size_t)ymin * src_stride + (size_t)xx * S;
   int acc[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) acc[c] = 1 << (kResamplePrec - 1);
@@ -105,40 +107,49 @@ __global__ __launch_bounds__(256) void resample_v_kernel(const uint8_t* __restri
 
 // No vertical resampling (ih == oh): convert the (horizontally resampled or original) rows.
 __global__ __launch_bounds__(256) void to_planar_f32_kernel(const uint8_t* __restrict__ src, int src_stride, int C,
-                                                           int oh, int ow, float* __restrict__ out) {
+                                                           int S, int oh, int ow, float* __restrict__ out) {
   const int xx = blockIdx.x * 256 + threadIdx.x;
   const int yy = blockIdx.y;
   if (xx >= ow || yy >= oh) return;
-  const uint8_t* p = src + (size_t)yy * src_stride + (size_t)xx * C;
+  const uint8_t* p = src + (size_t)yy * src_stride + (size_t)xx * S;
   const size_t plane = (size_t)oh * ow, o = (size_t)yy * ow + xx;
   for (int c = 0; c < 3; ++c) out[c * plane + o] = (float)p[C == 3 ? c : 0] / 255.0f;
 }
 
-hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int C, uint8_t* tmp, float* out,
+// channels: 1 (L), 3 (RGB) or 4 (RGBX: 3 channels, 4 bytes per pixel)
+hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int channels, uint8_t* tmp, float* out,
                            hipStream_t s) {
-  if ((C != 1 && C != 3) || p.oh <= 0 || p.ow <= 0) return hipErrorInvalidValue;
+  if ((channels != 1 && channels != 3 && channels != 4) || p.oh <= 0 || p.ow <= 0) return hipErrorInvalidValue;
+  const int C = channels == 1 ? 1 : 3, S = channels;
   const uint8_t* src = img;
-  int stride = p.iw * C;
+  int stride = p.iw * S, sstep = S;
   if (p.need_h) {
     const dim3 grid((unsigned)((p.ow + 255) / 256), (unsigned)p.h_rows);
-    if (C == 3)
-      hipLaunchKernelGGL(resample_h_kernel<3>, grid, dim3(256), 0, s, img, p.iw * C, p.h_y0, p.h_rows, p.h_bounds,
+    if (S == 4)
+      hipLaunchKernelGGL((resample_h_kernel<3, 4>), grid, dim3(256), 0, s, img, stride, p.h_y0, p.h_rows, p.h_bounds,
+                         p.h_kk, p.h_ksize, p.ow, tmp);
+    else if (S == 3)
+      hipLaunchKernelGGL((resample_h_kernel<3, 3>), grid, dim3(256), 0, s, img, stride, p.h_y0, p.h_rows, p.h_bounds,
                          p.h_kk, p.h_ksize, p.ow, tmp);
     else
-      hipLaunchKernelGGL(resample_h_kernel<1>, grid, dim3(256), 0, s, img, p.iw * C, p.h_y0, p.h_rows, p.h_bounds,
+      hipLaunchKernelGGL((resample_h_kernel<1, 1>), grid, dim3(256), 0, s, img, stride, p.h_y0, p.h_rows, p.h_bounds,
                          p.h_kk, p.h_ksize, p.ow, tmp);
-    src = tmp;
+    src = tmp;   // C bytes per pixel
     stride = p.ow * C;
+    sstep = C;
   }
   const dim3 grid((unsigned)((p.ow + 255) / 256), (unsigned)p.oh);
-  if (p.need_v && C == 3)
-    hipLaunchKernelGGL(resample_v_kernel<3>, grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize, p.oh,
-                       p.ow, out);
+  if (p.need_v && sstep == 4)
+    hipLaunchKernelGGL((resample_v_kernel<3, 4>), grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize,
+                       p.oh, p.ow, out);
+  else if (p.need_v && sstep == 3)
+    hipLaunchKernelGGL((resample_v_kernel<3, 3>), grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize,
+                       p.oh, p.ow, out);
   else if (p.need_v)
-    hipLaunchKernelGGL(resample_v_kernel<1>, grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize, p.oh,
-                       p.ow, out);
+    hipLaunchKernelGGL((resample_v_kernel<1, 1>), grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize,
+                       p.oh, p.ow, out);
   else
-    hipLaunchKernelGGL(to_planar_f32_kernel, grid, dim3(256), 0, s, src, stride, C, p.oh, p.ow, out);
+    hipLaunchKernelGGL(to_planar_f32_kernel, grid, dim3(256), 0, s, src, stride, C, sstep, p.oh, p.ow, out);
   return hipGetLastError();
 }
 
@@ -166,7 +177,7 @@ __device__ __forceinline__ void crop_rect(const int* b, int ih, int iw, int bh, 
   y2 = min(ih, y2 + py);
 }
 
-__global__ __launch_bounds__(256) void crop_stats_kernel(const uint8_t* __restrict__ img, int ih, int iw, int C,
+__global__ __launch_bounds__(256) void crop_stats_kernel(const uint8_t* __restrict__ img, int ih, int iw, int S,
                                                         const int* __restrict__ boxes, int bh, int bw, double pad,
                                                         int* __restrict__ rects,
                                                         unsigned long long* __restrict__ sums) {
@@ -185,11 +196,11 @@ __global__ __launch_bounds__(256) void crop_stats_kernel(const uint8_t* __restri
     rects[4 * i + 3] = y2;
   }
   if (x2 <= x1 || y2 <= y1) return;
-  const int rowlen = (x2 - x1) * C;
+  const int rowlen = (x2 - x1) * S;
   unsigned long long acc = 0;
   for (int y = y1 + (int)blockIdx.x; y < y2; y += (int)gridDim.x) {
-    const uint8_t* row = img + ((size_t)y * iw + x1) * C;
-    for (int k = threadIdx.x; k < rowlen; k += 256) acc += row[k];
+    const uint8_t* row = img + ((size_t)y * iw + x1) * S;
+    for (int k = threadIdx.x; k < rowlen; k += 256) acc += (S == 4 && (k & 3) == 3) ? 0u : row[k];   // RGBX: not X
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   if ((threadIdx.x & 63) == 0 && acc) atomicAdd(sums + i, acc);
@@ -197,7 +208,7 @@ __global__ __launch_bounds__(256) void crop_stats_kernel(const uint8_t* __restri
 
 hipError_t launch_crop_stats(const uint8_t* img, int ih, int iw, int C, const int* boxes, int n_boxes, int bh, int bw,
                              double pad, int* rects, unsigned long long* sums, hipStream_t s) {
-  if ((C != 1 && C != 3) || ih <= 0 || iw <= 0 || bh <= 0 || bw <= 0 || n_boxes <= 0) return hipErrorInvalidValue;
+  if ((C != 1 && C != 3 && C != 4) || ih <= 0 || iw <= 0 || bh <= 0 || bw <= 0 || n_boxes <= 0) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(sums, 0, (size_t)n_boxes * sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
   const int rows_per = 8;

@@ -10,13 +10,15 @@ Differences are internal only:
   * the per-field bounding boxes (np.where -> min/max, inference.py:84-90) are computed
     on the GPU too (unet_forward_boxes); the scale / 15 % pad / crop stays on the host;
   * RGB / L photos are resized on the GPU (unet_preprocess, bit-exact with Pillow's
-    BICUBIC resize), so only the original uint8 photo crosses PCIe;
+    BICUBIC resize), so only the original uint8 photo crosses PCIe (an RGB photo as Pillow's own
+    RGBX pixels, copied out without repacking);
   * for RGB / L photos the call's device work -- photo upload, resize, forward with masks and
     boxes, crop statistics and the copies back -- is one hipGraph per photo geometry
     (unet_photo_graph_create), replayed with one host call and one synchronisation.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import threading
 from collections import OrderedDict
@@ -141,6 +143,54 @@ def photo_array(pil_img: Image.Image) -> np.ndarray:
     return np.frombuffer(data, np.uint8).reshape(shape)
 
 
+class _ArrowArray(ctypes.Structure):
+    """The Arrow C data interface's ArrowArray (a stable ABI)."""
+
+
+_ArrowArray._fields_ = [("length", ctypes.c_int64), ("null_count", ctypes.c_int64), ("offset", ctypes.c_int64),
+                        ("n_buffers", ctypes.c_int64), ("n_children", ctypes.c_int64),
+                        ("buffers", ctypes.POINTER(ctypes.c_void_p)),
+                        ("children", ctypes.POINTER(ctypes.POINTER(_ArrowArray))),
+                        ("dictionary", ctypes.POINTER(_ArrowArray)), ("release", ctypes.c_void_p),
+                        ("private_data", ctypes.c_void_p)]
+_capsule_pointer = ctypes.pythonapi.PyCapsule_GetPointer
+_capsule_pointer.restype = ctypes.c_void_p
+_capsule_pointer.argtypes = [ctypes.py_object, ctypes.c_char_p]
+
+
+def copy_rgbx(pil_img: Image.Image, dst_ptr: int, capacity: int):
+    """Copy an "RGB" photo's pixels as Pillow holds them -- RGBX, 4 bytes per pixel -- to dst_ptr, without
+    the 3-byte repacking np.asarray does (about 60 us of a 600x400 photo on the GPU box's host): through
+    Pillow's zero-copy Arrow export of the image (a fixed-size list of 4 uint8 per pixel, one memory block).
+    Returns (H, W, 4), or None when the export is not available -- another mode (Pillow's export of "L"
+    images is not used: it crashes in Pillow 12), an image split over several memory blocks, an older
+    Pillow -- and the caller packs the photo instead."""
+    if pil_img.mode != "RGB":
+        return None
+    w, h = pil_img.size
+    n = w * h * 4
+    if n == 0 or n > capacity:
+        return None
+    try:
+        pil_img.load()
+        cap = pil_img.im.__arrow_c_array__()
+    except (AttributeError, ValueError, TypeError):
+        return None
+    try:
+        a = ctypes.cast(_capsule_pointer(cap, b"arrow_array"), ctypes.POINTER(_ArrowArray)).contents
+        if a.length != w * h or a.n_children != 1 or a.offset != 0:
+            return None
+        c = a.children[0].contents
+        if c.length != n or c.offset != 0 or c.n_buffers < 2 or not c.buffers[1]:
+            return None
+        ctypes.memmove(dst_ptr, c.buffers[1], n)
+    except (ValueError, TypeError):
+        return None
+    finally:
+        del cap   # the capsule's destructor releases the export (Pillow keeps the image alive until then)
+    return (h, w, 4)
+
+
 class _Staging:
     """Buffers of one device's run_unet calls, reused across calls: the photo (pinned host + device),
     the network input, the u8 masks and boxes, the crop statistics (device + pinned host), so a call
@@ -174,6 +224,22 @@ class _Staging:
             self.d_img = torch.empty(self.h_img.numel(), dtype=torch.uint8, device=self.device)
         self.h_img[:n].numpy()[:] = arr.reshape(-1)
         return self.d_img[:n].view(arr.shape)
+
+    def stage_photo(self, pil_img: Image.Image):
+        """The photo into the pinned host buffer: "RGB" as Pillow's RGBX pixels (copy_rgbx), else (and when
+        that export is unavailable) packed by photo_array.  Returns (device view it is uploaded to, channel
+        count of the crop statistics: 3 or 1)."""
+        w, h = pil_img.size
+        if pil_img.mode == "RGB":
+            if self.h_img is None or self.h_img.numel() < w * h * 4:
+                self.drop_graphs()
+                self.h_img = torch.empty(max(w * h * 4, 1 << 20), dtype=torch.uint8).pin_memory()
+                self.d_img = torch.empty(self.h_img.numel(), dtype=torch.uint8, device=self.device)
+            shape = copy_rgbx(pil_img, self.h_img.data_ptr(), self.h_img.numel())
+            if shape is not None:
+                return self.d_img[:w * h * 4].view(shape), 3
+        arr = photo_array(pil_img)
+        return self.stage(arr), (3 if arr.ndim == 3 else 1)
 
     def upload(self, arr: np.ndarray) -> torch.Tensor:
         """uint8 [H, W(, C)] host photo -> device tensor of the same shape (pinned, async)."""
@@ -225,8 +291,7 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
             # inference.py:63-64 (Pillow-exact BICUBIC resize + convert("RGB") + /255), the forward with the
             # fused sigmoid + threshold + per-field boxes, and the crop statistics, all on the device as
             # one graph per photo geometry: one launch, one synchronisation
-            arr = photo_array(pil_img)
-            img = st.stage(arr)
+            img, ch = st.stage_photo(pil_img)
             g = st.photo_graph(model, img)
             try:
                 g.launch(stream.cuda_stream)
@@ -236,7 +301,7 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
                 st.photo_graph(model, img).launch(stream.cuda_stream)
             stream.synchronize()
             m = st.hm.numpy()[0].view(np.bool_).copy()   # the kernel writes 0 / 1 bytes
-            rects, sums, ch = st.hr.numpy().copy(), st.hs.numpy().copy(), (3 if arr.ndim == 3 else 1)
+            rects, sums = st.hr.numpy().copy(), st.hs.numpy().copy()
             masks = {k: m[i] for i, k in enumerate(FIELDS)}
             return masks, {k: crop_from_stats(pil_img, rects[i], sums[i], ch) for i, k in enumerate(FIELDS)}
         # other PIL modes (RGBA premultiplied resize, P nearest, ...): the reference's host path
