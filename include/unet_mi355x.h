@@ -209,7 +209,6 @@ int unet_graph_create(unet_handle* h, const void* x, int x_layout, int x_dtype,
                       int N, int H, int W, unet_graph** out);
 int unet_graph_launch(unet_graph* g, void* hip_stream);
 int unet_graph_destroy(unet_graph* g);
-int unet_graph_wait_stats(unet_graph* g);
 
 /* One graph per photo geometry: the whole device part of run_unet (inference.py:58-129) -- the
  * upload of the pinned host photo (h_img; NULL: the caller fills img), unet_preprocess to size x size
@@ -218,10 +217,7 @@ int unet_graph_wait_stats(unet_graph* g);
  * rects, sums as there) and the copies of masks, boxes, rects and sums into the pinned host buffers
  * given (each may be NULL) -- captured once and replayed by unet_graph_launch: one host call and one
  * stream synchronisation per photo.  Needs unet_reserve(h, 1, size, size) first; stale (UNET_ESTATE at
- * launch) under the same rules as unet_graph_create's graphs.  Destroy with unet_graph_destroy.
- * The boxes / rects / sums copies come before the masks' copy; unet_graph_wait_stats(g) returns once
- * those are on the host (the caller builds the crops while the masks are still being copied), UNET_ESTATE
- * for a graph without host copies of both. */
+ * launch) under the same rules as unet_graph_create's graphs.  Destroy with unet_graph_destroy. */
 int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih, int iw, int channels, float* x,
                             int size, void* masks, int mask_kind, int32_t* boxes, double pad, int32_t* rects,
                             uint64_t* sums, void* h_masks, void* h_boxes, void* h_rects, void* h_sums,

@@ -1140,7 +1140,6 @@ def test_run_unet_photo_graphs_equal_eager_calls():
                 _same_result(inf.run_unet(p, ck, compute_dtype="mixed"), w, inf.FIELDS)
         st = inf._staging[str(inf.DEVICE)]
         assert 1 <= len(st.graphs) <= st.MAX_GRAPHS
-        print("photo graphs with the statistics event:", [g.wait_stats() for _, g in st.graphs.values()])
         inf.run_unet_batch(photos[:2], ck, compute_dtype="mixed", exact=False)   # may grow the workspace
         model.native_handle(dev).reserve(8, 512, 512)                          # grows it: graphs stale
         for p, w in zip(photos, want):

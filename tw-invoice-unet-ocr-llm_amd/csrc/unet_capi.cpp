@@ -147,8 +147,6 @@ struct unet_graph {
   // the graph (the handle's geometry cache may evict its own copy without staling the graph)
   ResampleStore rs;
   uint8_t* pp_tmp = nullptr;
-  // recorded after the boxes / crop statistics reach the host, before the masks' copy (unet_graph_wait_stats)
-  hipEvent_t stats_ev = nullptr;
 };
 
 namespace {
@@ -1409,57 +1407,35 @@ int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih
     hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
     if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
-  if (!rc && (h_boxes || h_rects || h_sums) && h_masks) {
-    hipError_t e = hipEventCreateWithFlags(&gr->stats_ev, hipEventDisableTiming);
-    if (e != hipSuccess) gr->stats_ev = nullptr;   // optional: the caller then waits for the whole graph
-  }
-  // the capture; tried once more without the statistics event should the runtime refuse an event record
-  // inside a capture
-  auto capture = [&]() -> int {
-    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
-    if (e != hipSuccess) return fail(UNET_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
-    int r = UNET_OK;
-    h->capturing = true;
-    const size_t img_bytes = (size_t)ih * iw * channels;
-    const int ncls = h->cfg.n_classes;
-    if (h_img) e = hipMemcpyAsync(img, h_img, img_bytes, hipMemcpyHostToDevice, cs);   // the photo upload
-    if (e == hipSuccess) e = launch_resample(p, static_cast<const uint8_t*>(img), channels, gr->pp_tmp, x, cs);
-    if (e != hipSuccess) r = fail(UNET_EHIP, std::string("photo graph upload / resize: ") + hipGetErrorString(e));
-    if (!r) r = forward_impl(h, x, UNET_LAYOUT_NCHW, UNET_IN_F32, nullptr, masks, mask_kind, boxes, 1, size, size, cs, nullptr);
-    if (!r) {
-      e = launch_crop_stats(static_cast<const uint8_t*>(img), ih, iw, channels, boxes, ncls, size, size, pad, rects,
-                            reinterpret_cast<unsigned long long*>(sums), cs);
-      const size_t mbytes = (size_t)ncls * size * (mask_kind == UNET_MASK_BITS ? size / 8 : size);
-      if (e == hipSuccess && h_boxes) e = hipMemcpyAsync(h_boxes, boxes, (size_t)ncls * 16, hipMemcpyDeviceToHost, cs);
-      if (e == hipSuccess && h_rects) e = hipMemcpyAsync(h_rects, rects, (size_t)ncls * 16, hipMemcpyDeviceToHost, cs);
-      if (e == hipSuccess && h_sums) e = hipMemcpyAsync(h_sums, sums, (size_t)ncls * 8, hipMemcpyDeviceToHost, cs);
-      if (e == hipSuccess && gr->stats_ev) e = hipEventRecord(gr->stats_ev, cs);
-      if (e == hipSuccess && h_masks) e = hipMemcpyAsync(h_masks, masks, mbytes, hipMemcpyDeviceToHost, cs);
-      if (e != hipSuccess) r = fail(UNET_EHIP, std::string("photo graph crop stats / copies: ") + hipGetErrorString(e));
-    }
-    h->capturing = false;
-    hipGraph_t graph = nullptr;
-    e = hipStreamEndCapture(cs, &graph);
-    if (!r && e != hipSuccess) r = fail(UNET_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
-    if (!r) {
-      gr->graph = graph;
-      e = hipGraphInstantiate(&gr->exec, gr->graph, nullptr, nullptr, 0);
-      if (e != hipSuccess) r = fail(UNET_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
-    } else if (graph) {
-      (void)hipGraphDestroy(graph);
-    }
-    return r;
-  };
   if (!rc) {
-    rc = capture();
-    if (rc && gr->stats_ev) {
-      if (gr->exec) (void)hipGraphExecDestroy(gr->exec);
-      if (gr->graph) (void)hipGraphDestroy(gr->graph);
-      gr->exec = nullptr;
-      gr->graph = nullptr;
-      (void)hipEventDestroy(gr->stats_ev);
-      gr->stats_ev = nullptr;
-      rc = capture();
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) {
+      rc = fail(UNET_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
+    } else {
+      h->capturing = true;
+      const size_t img_bytes = (size_t)ih * iw * channels;
+      const int ncls = h->cfg.n_classes;
+      if (h_img) e = hipMemcpyAsync(img, h_img, img_bytes, hipMemcpyHostToDevice, cs);   // the photo upload
+      if (e == hipSuccess) e = launch_resample(p, static_cast<const uint8_t*>(img), channels, gr->pp_tmp, x, cs);
+      if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("photo graph upload / resize: ") + hipGetErrorString(e));
+      if (!rc) rc = forward_impl(h, x, UNET_LAYOUT_NCHW, UNET_IN_F32, nullptr, masks, mask_kind, boxes, 1, size, size, cs, nullptr);
+      if (!rc) {
+        e = launch_crop_stats(static_cast<const uint8_t*>(img), ih, iw, channels, boxes, ncls, size, size, pad, rects,
+                              reinterpret_cast<unsigned long long*>(sums), cs);
+        const size_t mbytes = (size_t)ncls * size * (mask_kind == UNET_MASK_BITS ? size / 8 : size);
+        if (e == hipSuccess && h_masks) e = hipMemcpyAsync(h_masks, masks, mbytes, hipMemcpyDeviceToHost, cs);
+        if (e == hipSuccess && h_boxes) e = hipMemcpyAsync(h_boxes, boxes, (size_t)ncls * 16, hipMemcpyDeviceToHost, cs);
+        if (e == hipSuccess && h_rects) e = hipMemcpyAsync(h_rects, rects, (size_t)ncls * 16, hipMemcpyDeviceToHost, cs);
+        if (e == hipSuccess && h_sums) e = hipMemcpyAsync(h_sums, sums, (size_t)ncls * 8, hipMemcpyDeviceToHost, cs);
+        if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("photo graph crop stats / copies: ") + hipGetErrorString(e));
+      }
+      h->capturing = false;
+      e = hipStreamEndCapture(cs, &gr->graph);
+      if (!rc && e != hipSuccess) rc = fail(UNET_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+      if (!rc) {
+        e = hipGraphInstantiate(&gr->exec, gr->graph, nullptr, nullptr, 0);
+        if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+      }
     }
   }
   if (cs) (void)hipStreamDestroy(cs);
@@ -1485,14 +1461,6 @@ int unet_graph_launch(unet_graph* gr, void* stream) {
   return UNET_OK;
 }
 
-int unet_graph_wait_stats(unet_graph* gr) {
-  if (!gr) return fail(UNET_EINVAL, "null graph");
-  if (!gr->stats_ev) return fail(UNET_ESTATE, "graph has no statistics event");
-  DeviceGuard g(gr->h->cfg.device);
-  HIP_TRY(hipEventSynchronize(gr->stats_ev));
-  return UNET_OK;
-}
-
 int unet_graph_destroy(unet_graph* gr) {
   if (!gr) return UNET_OK;
   DeviceGuard g(gr->h->cfg.device);
@@ -1501,7 +1469,6 @@ int unet_graph_destroy(unet_graph* gr) {
   if (gr->graph) (void)hipGraphDestroy(gr->graph);
   free_resample(gr->rs);
   if (gr->pp_tmp) (void)hipFree(gr->pp_tmp);
-  if (gr->stats_ev) (void)hipEventDestroy(gr->stats_ev);
   delete gr;
   return UNET_OK;
 }

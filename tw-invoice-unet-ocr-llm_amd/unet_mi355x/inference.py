@@ -298,16 +298,12 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
             except RuntimeError:   # stale (the cached model's workspace grew, e.g. run_unet_batch): capture again
                 st.graphs.pop(tuple(img.shape), None)
                 g.close()
-                g = st.photo_graph(model, img)
-                g.launch(stream.cuda_stream)
-            # the crops (inference.py:92-127) while the masks are still being copied back
-            if not g.wait_stats():
-                stream.synchronize()
-            rects, sums = st.hr.numpy().copy(), st.hs.numpy().copy()
-            crops = {k: crop_from_stats(pil_img, rects[i], sums[i], ch) for i, k in enumerate(FIELDS)}
+                st.photo_graph(model, img).launch(stream.cuda_stream)
             stream.synchronize()
             m = st.hm.numpy()[0].view(np.bool_).copy()   # the kernel writes 0 / 1 bytes
-            return {k: m[i] for i, k in enumerate(FIELDS)}, crops
+            rects, sums = st.hr.numpy().copy(), st.hs.numpy().copy()
+            masks = {k: m[i] for i, k in enumerate(FIELDS)}
+            return masks, {k: crop_from_stats(pil_img, rects[i], sums[i], ch) for i, k in enumerate(FIELDS)}
         # other PIL modes (RGBA premultiplied resize, P nearest, ...): the reference's host path
         x = preprocess(pil_img.resize((IMG_SIZE, IMG_SIZE)))      # inference.py:63-64
         model.forward_boxes(x, masks="u8", out=(st.m, st.b))

@@ -88,7 +88,6 @@ SIGNATURES = {
     "unet_graph_create": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _i, ctypes.POINTER(_vp)]),
     "unet_graph_launch": (_i, [_vp, _vp]),
     "unet_graph_destroy": (_i, [_vp]),
-    "unet_graph_wait_stats": (_i, [_vp]),
     "unet_comm_get_unique_id": (_i, [_vp]),
     "unet_comm_init": (_i, [_vp, _i, _i, _vp]),
     "unet_allgather": (_i, [_vp, _vp, _vp, _sz, _vp]),
@@ -422,11 +421,6 @@ class Graph:
     def launch(self, stream: int) -> None:
         with self.handle.lock:
             check(self.handle.lib.unet_graph_launch(self._g, stream), "unet_graph_launch")
-
-    def wait_stats(self) -> bool:
-        """Photo graphs: block until the last launch's boxes / crop statistics are on the host (the masks'
-        copy may still run); False when the graph has no such event (then synchronise the stream)."""
-        return self.handle.lib.unet_graph_wait_stats(self._g) == UNET_OK
 
     def close(self) -> None:
         if getattr(self, "_g", None):
