@@ -58,6 +58,12 @@ fi
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --detail-out gpurun_out/bench_$TAG.detail.json \
     > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 echo bench ok
+# the profiles of this pass against the bench line of the same box (tools/stamp_profiles.py)
+if [ "$MODE" != "bench-only" ]; then
+  python tools/stamp_profiles.py --tag $TAG --commit $COMMIT --stats gpurun_out/prof_$TAG/run_kernel_stats.csv \
+      --pmc gpurun_out/pmc_$TAG/summary.json --bench gpurun_out/bench_$TAG.json --out gpurun_out/stamp_$TAG.json \
+      > /dev/null && echo stamp ok
+fi
 timeout -k 10 300 python bench.py --size 1024 --batch 64 --dtype fp16 --steps 5 --warmup 3 --cpu-seconds 10 --no-latency \
     --no-strong --detail-out gpurun_out/bench_${TAG}_cfg5.detail.json > gpurun_out/bench_${TAG}_cfg5_fp16_1024.json 2> gpurun_out/bench_${TAG}_cfg5.err
 echo bench cfg5 ok
