@@ -215,8 +215,10 @@ int unet_graph_destroy(unet_graph* g);
  * (the graph owns its resize tables and row buffer, so the handle's geometry cache may evict its own
  * copy), unet_forward_boxes at N = 1 (masks / mask_kind / boxes as there), unet_crop_stats (pad,
  * rects, sums as there) and the copies of masks, boxes, rects and sums into the pinned host buffers
- * given (each may be NULL) -- captured once and replayed by unet_graph_launch: one host call and one
- * stream synchronisation per photo.  Needs unet_reserve(h, 1, size, size) first; stale (UNET_ESTATE at
+ * given (each may be NULL; copies whose device and host buffers both follow the previous one's in
+ * memory, e.g. masks | boxes | rects | sums carved from one device and one host block, are made
+ * as one) -- captured once and replayed by unet_graph_launch: one host call and one stream
+ * synchronisation per photo.  Needs unet_reserve(h, 1, size, size) first; stale (UNET_ESTATE at
  * launch) under the same rules as unet_graph_create's graphs.  Destroy with unet_graph_destroy. */
 int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih, int iw, int channels, float* x,
                             int size, void* masks, int mask_kind, int32_t* boxes, double pad, int32_t* rects,

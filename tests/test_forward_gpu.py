@@ -696,23 +696,28 @@ def _np_boxes(masks):
 def test_mask_boxes_match_numpy(kind):
     """Device per-(image, field) boxes (unet_forward_boxes) == np.where min/max of the masks the
     same forward produced (inference.py:84-90), with and without caller mask buffers; empty
-    masks (torch_default weights: logits ~ -4) give -1s; W = 48 exercises a 16-bit word row."""
+    masks (torch_default weights: logits ~ -4) give -1s; W = 48 exercises a 16-bit word row;
+    1280 x 1024 has more 1024-word strips than blocks per mask (blocks loop).  Every handle runs
+    three forwards (page, mirrored page, page again): the strips' sync entries must be back in
+    their idle state after each launch."""
     cases = [(syn.make_state_dict(0, 3, 3, "pretrained"), syn.invoice_pages(1000, 2, 512, 512, 3)),
              (syn.make_state_dict(1, 3, 3, "torch_default"), syn.invoice_pages(2, 1, 64, 64, 3)),
-             (syn.make_state_dict(5, 3, 3, "structured", out_bias=0.0), syn.uniform_batch(3, 3, 3, 32, 48))]
+             (syn.make_state_dict(5, 3, 3, "structured", out_bias=0.0), syn.uniform_batch(3, 3, 3, 32, 48)),
+             (syn.make_state_dict(0, 3, 3, "pretrained"), syn.invoice_pages(3, 1, 1280, 1024, 3))]
     for sd, x in cases:
         m = make_model(sd, 3, "mixed")
-        xd = torch.from_numpy(x).to(DEV)
-        with torch.no_grad():
-            ref_masks = m.forward_masks(xd).cpu().numpy().astype(bool)
-            got = m.forward_boxes(xd, masks=kind)
-        boxes = (got if kind is None else got[1]).cpu().numpy()
-        assert np.array_equal(boxes, _np_boxes(ref_masks))
-        if kind is not None:
-            mk = got[0].cpu().numpy()
-            if kind == "bits":
-                mk = np.unpackbits(mk, axis=-1, bitorder="little")
-            assert np.array_equal(mk.astype(bool), ref_masks)
+        for xd in (torch.from_numpy(x).to(DEV), torch.from_numpy(x[..., ::-1].copy()).to(DEV),
+                   torch.from_numpy(x).to(DEV)):
+            with torch.no_grad():
+                ref_masks = m.forward_masks(xd).cpu().numpy().astype(bool)
+                got = m.forward_boxes(xd, masks=kind)
+            boxes = (got if kind is None else got[1]).cpu().numpy()
+            assert np.array_equal(boxes, _np_boxes(ref_masks))
+            if kind is not None:
+                mk = got[0].cpu().numpy()
+                if kind == "bits":
+                    mk = np.unpackbits(mk, axis=-1, bitorder="little")
+                assert np.array_equal(mk.astype(bool), ref_masks)
         m.close()
 
 
@@ -936,6 +941,16 @@ def test_crop_stats_match_host_crop_rules(h, w, c):
             r4, s4 = torch.empty_like(rects), torch.empty_like(sums)
             native.crop_stats(img4, b, 512, 512, inf.CROP_PAD, r4, s4, torch.cuda.current_stream().cuda_stream)
             assert torch.equal(r4, rects) and torch.equal(s4, sums)
+        for off in (1, 3):   # a photo not 4-byte aligned (the kernel walks aligned words and masks the ends)
+            for img_u in (img, img4 if c == 3 else None):
+                if img_u is None:
+                    continue
+                blk = torch.empty(img_u.numel() + 8, dtype=torch.uint8, device=DEV)
+                v = blk[off:off + img_u.numel()].view(img_u.shape)
+                v.copy_(img_u)
+                ru, su = torch.empty_like(rects), torch.empty_like(sums)
+                native.crop_stats(v, b, 512, 512, inf.CROP_PAD, ru, su, torch.cuda.current_stream().cuda_stream)
+                assert torch.equal(ru, rects) and torch.equal(su, sums), off
         rects, sums = rects.cpu().numpy(), sums.cpu().numpy()
         for i, box in enumerate(boxes):
             if box[2] < 0:

@@ -108,6 +108,17 @@ def main():
                 torch.cuda.synchronize()
                 print(f"[{dtype}] {name:16s} host+sync {host:.4f} ms   device {e0.elapsed_time(e1) / 20:.4f} ms",
                       flush=True)
+            # the crops with Pillow's block cache on (freed image blocks are kept for reuse instead of
+            # returned to the OS: no page faults on the new crop's pixels)
+            crops = {k: inf.crop_from_stats(pil, st.hr.numpy()[i], st.hs.numpy()[i], 3) for i, k in enumerate(inf.FIELDS)}
+            print(f"[{dtype}] crop sizes " + ", ".join(f"{k}: {None if c is None else c.size}" for k, c in crops.items()))
+            prev = Image.core.get_blocks_max()
+            Image.core.set_blocks_max(8)
+            f = stages["crops"]
+            for _ in range(3):
+                f()
+            print(f"[{dtype}] crops with Pillow blocks_max 8: {med(f, args.calls):.4f} ms", flush=True)
+            Image.core.set_blocks_max(prev)
             with torch.no_grad():
                 x = st.x
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

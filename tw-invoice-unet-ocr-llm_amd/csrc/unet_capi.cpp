@@ -136,6 +136,10 @@ struct unet_handle {
   int ksplit_max = 32;
   int ksplit_force[21] = {};
   void* part = nullptr;   // the current forward's partial buffer (workspace region Buffers::part)
+  // mask-box sync entries (launch_mask_boxes: kSyncInts ints per (image, field), idle between
+  // launches), grown by unet_reserve
+  int* box_sync = nullptr;
+  int box_sync_n = 0;
 };
 
 struct unet_graph {
@@ -147,6 +151,7 @@ struct unet_graph {
   // the graph (the handle's geometry cache may evict its own copy without staling the graph)
   ResampleStore rs;
   uint8_t* pp_tmp = nullptr;
+  int* crop_sync = nullptr;   // the crop sums' sync entries (n_classes, zeroed at capture)
 };
 
 namespace {
@@ -554,6 +559,35 @@ void free_all(unet_handle* h) {
   if (h->ws) (void)hipFree(h->ws);
   h->ws = nullptr;
   h->ws_bytes = 0;
+  if (h->box_sync) (void)hipFree(h->box_sync);
+  h->box_sync = nullptr;
+  h->box_sync_n = 0;
+}
+
+// At least n idle mask-box sync entries (at least 1024: N * n_classes up to 1024 never reallocates).
+int ensure_box_sync(unet_handle* h, int n) {
+  if (n <= h->box_sync_n) return UNET_OK;
+  n = std::max(n, 1024);
+  std::vector<int> idle((size_t)n * kSyncInts, 0);
+  for (int i = 0; i < n; ++i) {
+    int* e = idle.data() + (size_t)i * kSyncInts;
+    e[0] = e[1] = 0x7FFFFFFF;
+    e[2] = e[3] = -1;
+  }
+  ++h->generation;   // graphs captured the old entries
+  drain(h);
+  if (h->box_sync) (void)hipFree(h->box_sync);
+  h->box_sync = nullptr;
+  h->box_sync_n = 0;
+  hipError_t e = hipMalloc((void**)&h->box_sync, idle.size() * sizeof(int));
+  if (e != hipSuccess) {
+    h->box_sync = nullptr;
+    return fail(UNET_ENOMEM, std::string("mask-box sync hipMalloc: ") + hipGetErrorString(e));
+  }
+  e = hipMemcpy(h->box_sync, idle.data(), idle.size() * sizeof(int), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return fail(UNET_EHIP, std::string("mask-box sync init: ") + hipGetErrorString(e));
+  h->box_sync_n = n;
+  return UNET_OK;
 }
 
 // ---- Pillow's resize coefficients (libImaging/Resample.c: precompute_coeffs +
@@ -1013,8 +1047,10 @@ int unet_reserve(unet_handle* h, int N, int H, int W) {
   int rc = check_geometry(h, N, H, W);
   if (rc) return rc;
   const size_t need = plan(h, N, H, W).total;
-  if (need <= h->ws_bytes) return UNET_OK;
   DeviceGuard g(h->cfg.device);
+  rc = ensure_box_sync(h, N * h->cfg.n_classes);
+  if (rc) return rc;
+  if (need <= h->ws_bytes) return UNET_OK;
   ++h->generation;
   if (h->ws) {
     drain(h);   // the old workspace may still be in use by queued forwards
@@ -1108,6 +1144,8 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   // no allocation (and so no hidden device synchronisation) here: unet_reserve sizes the workspace
   if (plan(h, N, H, W).total > h->ws_bytes)
     return fail(UNET_ESTATE, "workspace too small for this (N, H, W): call unet_reserve first");
+  if (boxes && N * h->cfg.n_classes > h->box_sync_n)
+    return fail(UNET_ESTATE, "mask-box sync entries too few for this N: call unet_reserve first");
   DeviceGuard g(h->cfg.device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   order_after_last(h, s);
@@ -1186,7 +1224,7 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
 #undef RUN
   if (boxes) {   // per-(image, field) mask bounding boxes (inference.py:84-90)
     hipError_t e = launch_mask_boxes(static_cast<const uint8_t*>(masks), mask_kind, N, h->cfg.n_classes, H, W,
-                                     boxes, s);
+                                     boxes, h->box_sync, s);
     if (e != hipSuccess) return fail(UNET_EHIP, std::string("mask boxes launch: ") + hipGetErrorString(e));
   }
   mark();
@@ -1263,7 +1301,7 @@ int unet_crop_stats(const void* img, int ih, int iw, int channels, const int32_t
       n_boxes > 65535 || !(pad >= 0.0 && pad < 1.0))
     return fail(UNET_EINVAL, "bad image size, box geometry, box count or pad");
   hipError_t e = launch_crop_stats(static_cast<const uint8_t*>(img), ih, iw, channels, boxes, n_boxes, box_h, box_w,
-                                   pad, rects, reinterpret_cast<unsigned long long*>(sums),
+                                   pad, rects, reinterpret_cast<unsigned long long*>(sums), nullptr,
                                    static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return fail(UNET_EHIP, std::string("crop stats launch: ") + hipGetErrorString(e));
   return UNET_OK;
@@ -1402,6 +1440,12 @@ int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih
     hipError_t e = hipMalloc((void**)&gr->pp_tmp, tmp);
     if (e != hipSuccess) rc = fail(UNET_ENOMEM, std::string("preprocess buffer: ") + hipGetErrorString(e));
   }
+  if (!rc) {   // the crop sums' sync entries, idle (zero)
+    const size_t bytes = (size_t)h->cfg.n_classes * kSyncInts * sizeof(int);
+    hipError_t e = hipMalloc((void**)&gr->crop_sync, bytes);
+    if (e == hipSuccess) e = hipMemset(gr->crop_sync, 0, bytes);
+    if (e != hipSuccess) rc = fail(UNET_ENOMEM, std::string("crop sync entries: ") + hipGetErrorString(e));
+  }
   hipStream_t cs = nullptr;
   if (!rc) {
     hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
@@ -1421,12 +1465,27 @@ int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih
       if (!rc) rc = forward_impl(h, x, UNET_LAYOUT_NCHW, UNET_IN_F32, nullptr, masks, mask_kind, boxes, 1, size, size, cs, nullptr);
       if (!rc) {
         e = launch_crop_stats(static_cast<const uint8_t*>(img), ih, iw, channels, boxes, ncls, size, size, pad, rects,
-                              reinterpret_cast<unsigned long long*>(sums), cs);
+                              reinterpret_cast<unsigned long long*>(sums), gr->crop_sync, cs);
+        // the copies back, adjacent ones (device and host both contiguous) merged: each copy node
+        // costs about 4.5 us, whatever its size
         const size_t mbytes = (size_t)ncls * size * (mask_kind == UNET_MASK_BITS ? size / 8 : size);
-        if (e == hipSuccess && h_masks) e = hipMemcpyAsync(h_masks, masks, mbytes, hipMemcpyDeviceToHost, cs);
-        if (e == hipSuccess && h_boxes) e = hipMemcpyAsync(h_boxes, boxes, (size_t)ncls * 16, hipMemcpyDeviceToHost, cs);
-        if (e == hipSuccess && h_rects) e = hipMemcpyAsync(h_rects, rects, (size_t)ncls * 16, hipMemcpyDeviceToHost, cs);
-        if (e == hipSuccess && h_sums) e = hipMemcpyAsync(h_sums, sums, (size_t)ncls * 8, hipMemcpyDeviceToHost, cs);
+        struct Copy { char* dst; const char* src; size_t bytes; };
+        std::vector<Copy> copies;
+        auto add = [&](void* dst, const void* src, size_t bytes) {
+          if (!dst) return;
+          char* d = static_cast<char*>(dst);
+          const char* sp = static_cast<const char*>(src);
+          if (!copies.empty() && copies.back().dst + copies.back().bytes == d && copies.back().src + copies.back().bytes == sp)
+            copies.back().bytes += bytes;
+          else
+            copies.push_back({d, sp, bytes});
+        };
+        add(h_masks, masks, mbytes);
+        add(h_boxes, boxes, (size_t)ncls * 16);
+        add(h_rects, rects, (size_t)ncls * 16);
+        add(h_sums, sums, (size_t)ncls * 8);
+        for (const Copy& c : copies)
+          if (e == hipSuccess) e = hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToHost, cs);
         if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("photo graph crop stats / copies: ") + hipGetErrorString(e));
       }
       h->capturing = false;
@@ -1469,6 +1528,7 @@ int unet_graph_destroy(unet_graph* gr) {
   if (gr->graph) (void)hipGraphDestroy(gr->graph);
   free_resample(gr->rs);
   if (gr->pp_tmp) (void)hipFree(gr->pp_tmp);
+  if (gr->crop_sync) (void)hipFree(gr->crop_sync);
   delete gr;
   return UNET_OK;
 }

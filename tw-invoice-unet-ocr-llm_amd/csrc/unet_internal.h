@@ -156,12 +156,20 @@ struct ResamplePlan {
 hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int C, uint8_t* tmp, float* out,
                            hipStream_t s);
 
-// per-(image, field) mask bounding boxes [N*ncls][4] = x_min, y_min, x_max, y_max (-1s if empty)
+// Cross-block reductions (mask boxes, crop sums) meet in "sync entries" of kSyncInts ints: the
+// blocks' atomics plus a block counter; the last block writes the result and restores the idle
+// state, so an entry is initialised once (init_box_sync / zeroed) and then reused by every launch.
+constexpr int kSyncInts = 8;
+// Idle state: mask-box entry {INT_MAX, INT_MAX, -1, -1, 0, 0, 0, 0}; crop-sum entry all zero.
+
+// per-(image, field) mask bounding boxes [N*ncls][4] = x_min, y_min, x_max, y_max (-1s if empty);
+// sync: N*ncls idle mask-box entries
 constexpr int kMaxBoxW = 16384;
-hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, int H, int W, int* boxes,
+hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, int H, int W, int* boxes, int* sync,
                              hipStream_t s);
-// crop rectangles + crop pixel sums of mask boxes on the device photo (unet_preprocess.hip)
+// crop rectangles + crop pixel sums of mask boxes on the device photo (unet_preprocess.hip);
+// sync: n_boxes zeroed entries, or NULL (sums are then cleared by a memset node and accumulated in place)
 hipError_t launch_crop_stats(const uint8_t* img, int ih, int iw, int C, const int* boxes, int n_boxes, int bh, int bw,
-                             double pad, int* rects, unsigned long long* sums, hipStream_t s);
+                             double pad, int* rects, unsigned long long* sums, int* sync, hipStream_t s);
 
 }  // namespace unet

@@ -21,6 +21,7 @@
 //    zero-copy: producers write straight into channel halves of one NHWC buffer.
 #include "unet_internal.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace unet {
@@ -2837,13 +2838,16 @@ hipError_t launch_splitk_reduce(DType to, DType tq, int epi, const IgemmArgs& a,
 // ---------------------------------------------------------------------------------
 // per-(image, field) bounding box of a mask: inference.py:84-90 (np.where(mask) ->
 // xs.min(), xs.max(), ys.min(), ys.max()) on the GPU, 4 ints instead of H*W host bytes.
-// One 1024-thread block per (n, c).  The mask is walked as 16-pixel column words (bit j of word
-// w = pixel 16*w + j: a little-endian 16-bit word of a bit-packed mask, or 16 bytes of a uint8
-// mask reduced to their nonzero bits); thread t takes words t, t + 1024, ..., so with W / 16
-// dividing 1024 it always sees the same column word and ORs it in a register (one LDS atomic per
-// thread instead of one per set pixel), and keeps the first / last row with a set bit.  Eight
-// loads are in flight per thread: a 512x512 uint8 plane is two rounds of memory latency (with 256
-// threads and four loads it was sixteen, 29 us per batch-1 call).  Empty mask -> (-1,-1,-1,-1).
+// Blocks (n, c) x strips: each 256-thread block walks strips of 1024 16-pixel column words (bit j of
+// word w = pixel 16*w + j: a little-endian 16-bit word of a bit-packed mask, or 16 bytes of a uint8
+// mask reduced to their nonzero bits), four loads in flight per thread; with W / 16 dividing 256 a
+// thread always sees the same column word and ORs it in a register (one LDS atomic per thread
+// instead of one per set pixel), and keeps the first / last row with a set bit.  The strips' boxes
+// meet in the handle's sync entry of (n, c) (device-scope atomics); the block that counts last
+// writes the box and resets the entry to its idle state {INT_MAX, INT_MAX, -1, -1, 0}, so the next
+// launch (or graph replay) needs no clearing pass.  One block per mask was 18.6 us per batch-1
+// call: a single CU cannot keep enough loads in flight to pull a 256 KB plane faster.
+// Empty mask -> (-1,-1,-1,-1).
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ unsigned nz_bits4(unsigned d) {   // bit j = byte j of d nonzero
   d |= d >> 4;
@@ -2852,11 +2856,11 @@ __device__ __forceinline__ unsigned nz_bits4(unsigned d) {   // bit j = byte j o
   return (d & 1u) | ((d >> 7) & 2u) | ((d >> 14) & 4u) | ((d >> 21) & 8u);
 }
 
-constexpr int kBoxThreads = 1024, kBoxLoads = 8;
+constexpr int kBoxThreads = 256, kBoxLoads = 4, kBoxChunk = kBoxThreads * kBoxLoads, kBoxMaxStrips = 64;
 
 template <int KIND, bool VEC>
 __global__ __launch_bounds__(kBoxThreads) void mask_boxes_kernel(const uint8_t* __restrict__ masks, int H, int W,
-                                                        int* __restrict__ boxes) {
+                                                        int* __restrict__ boxes, int* __restrict__ sync) {
   __shared__ unsigned col_or[kMaxBoxW / 16];
   __shared__ int ymin_s, ymax_s, xmin_s, xmax_s;
   const int tid = threadIdx.x;
@@ -2865,6 +2869,7 @@ __global__ __launch_bounds__(kBoxThreads) void mask_boxes_kernel(const uint8_t* 
   if (tid == 0) { ymin_s = 0x7FFFFFFF; ymax_s = -1; xmin_s = 0x7FFFFFFF; xmax_s = -1; }
   __syncthreads();
   const int total = H * words;
+  const int chunks = (total + kBoxChunk - 1) / kBoxChunk;
   const size_t plane = KIND == MASK_BITS ? (size_t)H * (W / 8) : (size_t)H * W;
   const uint8_t* base = masks + (size_t)blockIdx.x * plane;
   auto word_at = [&](int i) -> unsigned {   // 16-pixel column word i of the plane
@@ -2881,7 +2886,8 @@ __global__ __launch_bounds__(kBoxThreads) void mask_boxes_kernel(const uint8_t* 
   };
   int ymin = 0x7FFFFFFF, ymax = -1, cw = -1;
   unsigned cacc = 0;
-  for (int i0 = tid; i0 < total; i0 += kBoxLoads * kBoxThreads) {
+  for (int c = blockIdx.y; c < chunks; c += gridDim.y) {
+    const int i0 = c * kBoxChunk + tid;
     unsigned v[kBoxLoads];
 #pragma unroll
     for (int k = 0; k < kBoxLoads; ++k) v[k] = i0 + k * kBoxThreads < total ? word_at(i0 + k * kBoxThreads) : 0u;
@@ -2914,25 +2920,41 @@ __global__ __launch_bounds__(kBoxThreads) void mask_boxes_kernel(const uint8_t* 
   }
   __syncthreads();
   if (tid == 0) {
-    int* b = boxes + (size_t)blockIdx.x * 4;
-    const bool any = ymax_s >= 0;
-    b[0] = any ? xmin_s : -1;
-    b[1] = any ? ymin_s : -1;
-    b[2] = any ? xmax_s : -1;
-    b[3] = any ? ymax_s : -1;
+    int* e = sync + (size_t)blockIdx.x * kSyncInts;   // x_min, y_min, x_max, y_max, strips counted
+    if (ymax_s >= 0) {
+      atomicMin(e, xmin_s);
+      atomicMin(e + 1, ymin_s);
+      atomicMax(e + 2, xmax_s);
+      atomicMax(e + 3, ymax_s);
+    }
+    __threadfence();
+    if (atomicAdd(reinterpret_cast<unsigned*>(e + 4), 1u) == gridDim.y - 1) {   // the last strip of (n, c)
+      __threadfence();
+      const int x0 = atomicExch(e, 0x7FFFFFFF), y0 = atomicExch(e + 1, 0x7FFFFFFF);
+      const int x1 = atomicExch(e + 2, -1), y1 = atomicExch(e + 3, -1);
+      atomicExch(e + 4, 0);
+      int* b = boxes + (size_t)blockIdx.x * 4;
+      const bool any = y1 >= 0;
+      b[0] = any ? x0 : -1;
+      b[1] = any ? y0 : -1;
+      b[2] = any ? x1 : -1;
+      b[3] = any ? y1 : -1;
+    }
   }
 }
 
-hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, int H, int W, int* boxes,
+hipError_t launch_mask_boxes(const uint8_t* masks, int kind, int N, int ncls, int H, int W, int* boxes, int* sync,
                              hipStream_t s) {
-  if (W % 16 || W > kMaxBoxW || (kind != MASK_BITS && kind != MASK_U8)) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)(N * ncls)), block(kBoxThreads);
+  if (W % 16 || W > kMaxBoxW || (kind != MASK_BITS && kind != MASK_U8) || !sync) return hipErrorInvalidValue;
+  const long long chunks = ((long long)H * (W / 16) + kBoxChunk - 1) / kBoxChunk;
+  const dim3 grid((unsigned)(N * ncls), (unsigned)std::max(1LL, std::min<long long>(chunks, kBoxMaxStrips)));
+  const dim3 block(kBoxThreads);
   if (kind == MASK_BITS) {
-    hipLaunchKernelGGL((mask_boxes_kernel<MASK_BITS, false>), grid, block, 0, s, masks, H, W, boxes);
+    hipLaunchKernelGGL((mask_boxes_kernel<MASK_BITS, false>), grid, block, 0, s, masks, H, W, boxes, sync);
   } else if (reinterpret_cast<uintptr_t>(masks) % 16 == 0) {
-    hipLaunchKernelGGL((mask_boxes_kernel<MASK_U8, true>), grid, block, 0, s, masks, H, W, boxes);
+    hipLaunchKernelGGL((mask_boxes_kernel<MASK_U8, true>), grid, block, 0, s, masks, H, W, boxes, sync);
   } else {
-    hipLaunchKernelGGL((mask_boxes_kernel<MASK_U8, false>), grid, block, 0, s, masks, H, W, boxes);
+    hipLaunchKernelGGL((mask_boxes_kernel<MASK_U8, false>), grid, block, 0, s, masks, H, W, boxes, sync);
   }
   return hipGetLastError();
 }

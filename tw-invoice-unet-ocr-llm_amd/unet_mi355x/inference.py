@@ -204,15 +204,28 @@ class _Staging:
         self.lock = threading.Lock()
         self.h_img = self.d_img = None
         self.x = torch.empty((1, 3, IMG_SIZE, IMG_SIZE), dtype=torch.float32, device=self.device)
-        self.m = torch.empty((1, len(FIELDS), IMG_SIZE, IMG_SIZE), dtype=torch.uint8, device=self.device)
-        self.b = torch.empty((1, len(FIELDS), 4), dtype=torch.int32, device=self.device)
-        self.r = torch.empty((len(FIELDS), 4), dtype=torch.int32, device=self.device)   # crop rectangles
-        self.s = torch.empty((len(FIELDS),), dtype=torch.int64, device=self.device)     # crop pixel sums
-        self.hm = torch.empty(self.m.shape, dtype=torch.uint8).pin_memory()
-        self.hb = torch.empty(self.b.shape, dtype=torch.int32).pin_memory()
-        self.hr = torch.empty(self.r.shape, dtype=torch.int32).pin_memory()
-        self.hs = torch.empty(self.s.shape, dtype=torch.int64).pin_memory()
+        # the outputs, u8 masks | boxes | crop rectangles | crop pixel sums, carved from one device and
+        # one pinned host block in the same order: the photo graph copies them back as one
+        self.m, self.b, self.r, self.s = self._outputs(torch.empty(self._out_bytes(), dtype=torch.uint8,
+                                                                   device=self.device))
+        self.hm, self.hb, self.hr, self.hs = self._outputs(torch.empty(self._out_bytes(), dtype=torch.uint8).pin_memory())
         self.graphs: OrderedDict = OrderedDict()   # (ih, iw, c) -> (model, native.Graph)
+
+    @staticmethod
+    def _out_bytes():
+        n = len(FIELDS)
+        return n * IMG_SIZE * IMG_SIZE + n * 16 + n * 16 + n * 8
+
+    @staticmethod
+    def _outputs(block: torch.Tensor):
+        n = len(FIELDS)
+        o1 = n * IMG_SIZE * IMG_SIZE   # a multiple of 8: the int64 sums stay aligned
+        o2, o3 = o1 + n * 16, o1 + n * 32
+        m = block[:o1].view(1, n, IMG_SIZE, IMG_SIZE)
+        b = block[o1:o2].view(torch.int32).view(1, n, 4)
+        r = block[o2:o3].view(torch.int32).view(n, 4)
+        s = block[o3:o3 + n * 8].view(torch.int64)
+        return m, b, r, s
 
     def stage(self, arr: np.ndarray) -> torch.Tensor:
         """uint8 [H, W(, C)] host photo -> the pinned host buffer (grown when needed: the photo graphs
@@ -260,8 +273,10 @@ class _Staging:
         if e is not None and e[0] is model:
             self.graphs.move_to_end(key)
             return e[1]
-        if e is not None:
-            e[1].close()
+        if any(m is not model for m, _ in self.graphs.values()):
+            # another model (a re-loaded checkpoint or another precision plan): the model cache holds one
+            # model, so drop its graphs -- they keep its handle (workspace, weights) alive
+            self.drop_graphs()
         h = model.native_handle(self.device)
         h.reserve(1, IMG_SIZE, IMG_SIZE)
         img3 = img if img.dim() == 3 else img.unsqueeze(-1)
