@@ -212,8 +212,9 @@ int unet_graph_destroy(unet_graph* g);
 
 /* One graph per photo geometry: the whole device part of run_unet (inference.py:58-129) -- the
  * upload of the pinned host photo (h_img; NULL: the caller fills img), unet_preprocess to size x size
- * (the graph owns its resize tables and row buffer, so the handle's geometry cache may evict its own
- * copy), unet_forward_boxes at N = 1 (masks / mask_kind / boxes as there), unet_crop_stats (pad,
+ * into x (on the 16-bit plans, when the photo's height differs from size, the resize writes the first
+ * conv's pre-cast input into the workspace instead and x is not written; the graph owns its resize
+ * tables and row buffer, so the handle's geometry cache may evict its own copy), unet_forward_boxes at N = 1 (masks / mask_kind / boxes as there), unet_crop_stats (pad,
  * rects, sums as there) and the copies of masks, boxes, rects and sums into the pinned host buffers
  * given (each may be NULL; copies whose device and host buffers both follow the previous one's in
  * memory, e.g. masks | boxes | rects | sums carved from one device and one host block, are made

@@ -1120,17 +1120,23 @@ def test_run_unet_batch_exact_above_the_small_batch_limit():
             assert orc.mask_iou(m1[k], m2[k]) >= 0.999, k
 
 
-def test_run_unet_photo_graphs_equal_eager_calls():
+@pytest.mark.parametrize("dtype", ["mixed", "bf16"])
+def test_run_unet_photo_graphs_equal_eager_calls(dtype):
     """run_unet replays one photo graph per geometry (upload + resize + forward + boxes + crop statistics +
     copies back, unet_photo_graph_create).  Alternating geometries (RGB and L), a photo larger than the
     staging buffer (its graphs are re-captured over the new buffers) and a stale graph (the cached model's
-    workspace grown by a batch call) all return what the eager device path returns, bit for bit."""
+    workspace grown by a batch call) all return what the eager device path returns, bit for bit.  The
+    16-bit plans' graphs resize straight into the first conv's pre-cast input (fp16 / bf16) when the
+    photo's height is not 512; 512-high, 512-wide and 512 x 512 photos take the fp32 planes + pre-cast."""
     from unet_mi355x import inference as inf
-    photos = _photos(4) + [_photos(6)[5].resize((1800, 1400))]
+    extra = _photos(7)
+    photos = _photos(4) + [_photos(6)[5].resize((1800, 1400)), extra[6].resize((700, 512)),
+                           extra[6].resize((512, 300)), extra[6].resize((512, 512)),
+                           extra[6].convert("L").resize((333, 512))]
     with tempfile.TemporaryDirectory() as td:
         ck = _save_ckpt(td)
         inf.DEVICE = DEV
-        model = inf._cached_model(ck, "mixed")
+        model = inf._cached_model(ck, dtype)
         dev = torch.device(DEV)
 
         def eager(pil):   # the round-4 device path: separate preprocess / forward_boxes / crop_stats calls
@@ -1152,13 +1158,14 @@ def test_run_unet_photo_graphs_equal_eager_calls():
         want = [eager(p) for p in photos]
         for rep in range(2):
             for p, w in zip(photos, want):
-                _same_result(inf.run_unet(p, ck, compute_dtype="mixed"), w, inf.FIELDS)
+                _same_result(inf.run_unet(p, ck, compute_dtype=dtype), w, inf.FIELDS)
         st = inf._staging[str(inf.DEVICE)]
         assert 1 <= len(st.graphs) <= st.MAX_GRAPHS
-        inf.run_unet_batch(photos[:2], ck, compute_dtype="mixed", exact=False)   # may grow the workspace
-        model.native_handle(dev).reserve(8, 512, 512)                          # grows it: graphs stale
+        assert all(m is model for m, _ in st.graphs.values())   # another model's graphs were dropped
+        inf.run_unet_batch(photos[:2], ck, compute_dtype=dtype, exact=False)   # may grow the workspace
+        model.native_handle(dev).reserve(8, 512, 512)                        # grows it: graphs stale
         for p, w in zip(photos, want):
-            _same_result(inf.run_unet(p, ck, compute_dtype="mixed"), w, inf.FIELDS)
+            _same_result(inf.run_unet(p, ck, compute_dtype=dtype), w, inf.FIELDS)
 
 
 def test_launch_labels_at_name_the_small_batch_kernels():

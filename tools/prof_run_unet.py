@@ -64,6 +64,36 @@ def main():
             pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(22)
             print(s.getvalue(), flush=True)
 
+            # run_unet's RGB path step by step (the same calls), host time per section
+            secs = {}
+            for it in range(args.calls + 3):
+                t = [time.perf_counter()]
+                model_ = inf._cached_model(ck, dtype)
+                t.append(time.perf_counter())
+                st_ = inf._staging[str(inf.DEVICE)]
+                with st_.lock, torch.no_grad():
+                    stream_ = torch.cuda.current_stream(st_.device)
+                    t.append(time.perf_counter())
+                    img_, ch_ = st_.stage_photo(pil)
+                    t.append(time.perf_counter())
+                    g_ = st_.photo_graph(model_, img_)
+                    g_.launch(stream_.cuda_stream)
+                    t.append(time.perf_counter())
+                    stream_.synchronize()
+                    t.append(time.perf_counter())
+                    m_ = st_.hm.numpy()[0].view(np.bool_).copy()
+                    rects_, sums_ = st_.hr.numpy().copy(), st_.hs.numpy().copy()
+                    masks_ = {k: m_[i] for i, k in enumerate(inf.FIELDS)}
+                    t.append(time.perf_counter())
+                    crops_ = {k: inf.crop_from_stats(pil, rects_[i], sums_[i], ch_) for i, k in enumerate(inf.FIELDS)}
+                    t.append(time.perf_counter())
+                if it >= 3:
+                    for j, name in enumerate(["cached_model", "lock+no_grad+stream", "stage_photo", "graph lookup+launch",
+                                              "synchronize", "masks+rects copies", "crops"]):
+                        secs.setdefault(name, []).append(t[j + 1] - t[j])
+            print(f"[{dtype}] run_unet sections (median us): " +
+                  ", ".join(f"{k} {1e6 * float(np.median(v)):.1f}" for k, v in secs.items()), flush=True)
+
             # the stages of run_unet, each followed by a synchronisation
             model = inf._cached_model(ck, dtype)
             st = inf._staging[str(inf.DEVICE)]
@@ -119,6 +149,19 @@ def main():
                 f()
             print(f"[{dtype}] crops with Pillow blocks_max 8: {med(f, args.calls):.4f} ms", flush=True)
             Image.core.set_blocks_max(prev)
+            # the crops on worker threads (Pillow's crop copies rows with the GIL released)
+            from concurrent.futures import ThreadPoolExecutor
+            ex = ThreadPoolExecutor(2)
+            rr, ss = st.hr.numpy(), st.hs.numpy()
+
+            def pooled():
+                fs = [ex.submit(inf.crop_from_stats, pil, rr[i], ss[i], 3) for i in range(1, 3)]
+                c0 = inf.crop_from_stats(pil, rr[0], ss[0], 3)
+                return [c0] + [x.result() for x in fs]
+            for _ in range(3):
+                pooled()
+            print(f"[{dtype}] crops on 2 pool threads + caller: {med(pooled, args.calls):.4f} ms", flush=True)
+            ex.shutdown()
             with torch.no_grad():
                 x = st.x
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

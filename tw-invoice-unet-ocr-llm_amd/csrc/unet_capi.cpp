@@ -1131,8 +1131,11 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
 
 // The launch sequence of UNet.forward (unet_model.py:55-86).  ev (optional, kLaunches+1
 // events) brackets every launch for per-layer timing.
+// x_px4 (the photo graph): x is already the fused first conv's pre-cast input (launch_resample's
+// px4 output), so the pre-cast launch is skipped.
 int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void* logits, void* masks,
-                 int mask_kind, int32_t* boxes, int N, int H, int W, void* stream, hipEvent_t* ev) {
+                 int mask_kind, int32_t* boxes, int N, int H, int W, void* stream, hipEvent_t* ev,
+                 bool x_px4 = false) {
   if (!h || !x) return fail(UNET_EINVAL, "null argument");
   if (!h->loaded) return fail(UNET_ESTATE, "weights not loaded");
   if ((x_layout != UNET_LAYOUT_NCHW && x_layout != UNET_LAYOUT_NHWC) || (x_dtype != UNET_IN_F32 && x_dtype != UNET_IN_U8))
@@ -1166,11 +1169,12 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   // down1.net.0 (C -> 64): fused into down1.3 on the 16-bit ring path (fed by the pre-cast input),
   // a direct conv otherwise
   const void* x0 = x;
-  if (cfg_fused_in(h->L[D1B].cfg)) {
+  if (x_px4 && !cfg_fused_in(h->L[D1B].cfg)) return fail(UNET_EINVAL, "pre-cast input on a plan without the fused first conv");
+  if (cfg_fused_in(h->L[D1B].cfg) && !x_px4) {
     hipError_t e = launch_x_to_px4(h->L[D1B].dt, x, x_layout, x_dtype, N, C, H, W, buf(B.xpx), s);
     if (e != hipSuccess) return fail(UNET_EHIP, std::string("input pre-cast launch: ") + hipGetErrorString(e));
     x0 = buf(B.xpx);
-  } else {
+  } else if (!x_px4) {
     const float* xf = static_cast<const float*>(x);
     if (x_layout != UNET_LAYOUT_NCHW || x_dtype != UNET_IN_F32) {
       hipError_t e = launch_x_to_nchw_f32(x, x_layout, x_dtype, N, C, H, W, static_cast<float*>(buf(B.xpx)), s);
@@ -1459,10 +1463,18 @@ int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih
       h->capturing = true;
       const size_t img_bytes = (size_t)ih * iw * channels;
       const int ncls = h->cfg.n_classes;
+      // on the 16-bit plans with a vertical pass, the resize writes the fused first conv's pre-cast
+      // input straight into the workspace (one launch less; x is not written then)
+      const bool px4 = cfg_fused_in(h->L[D1B].cfg) && p.need_v;
+      void* xin = px4 ? static_cast<void*>(h->ws + plan(h, 1, size, size).xpx) : static_cast<void*>(x);
       if (h_img) e = hipMemcpyAsync(img, h_img, img_bytes, hipMemcpyHostToDevice, cs);   // the photo upload
-      if (e == hipSuccess) e = launch_resample(p, static_cast<const uint8_t*>(img), channels, gr->pp_tmp, x, cs);
+      if (e == hipSuccess)
+        e = launch_resample(p, static_cast<const uint8_t*>(img), channels, gr->pp_tmp, xin, cs,
+                            px4 ? h->L[D1B].dt : DType::F32);
       if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("photo graph upload / resize: ") + hipGetErrorString(e));
-      if (!rc) rc = forward_impl(h, x, UNET_LAYOUT_NCHW, UNET_IN_F32, nullptr, masks, mask_kind, boxes, 1, size, size, cs, nullptr);
+      if (!rc)
+        rc = forward_impl(h, xin, UNET_LAYOUT_NCHW, UNET_IN_F32, nullptr, masks, mask_kind, boxes, 1, size, size, cs,
+                          nullptr, px4);
       if (!rc) {
         e = launch_crop_stats(static_cast<const uint8_t*>(img), ih, iw, channels, boxes, ncls, size, size, pad, rects,
                               reinterpret_cast<unsigned long long*>(sums), gr->crop_sync, cs);

@@ -153,8 +153,10 @@ struct ResamplePlan {
   const int* h_bounds; const int* h_kk;
   const int* v_bounds; const int* v_kk;
 };
-hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int C, uint8_t* tmp, float* out,
-                           hipStream_t s);
+// out: fp32 planes [3][oh][ow]; px4 = F16 / BF16 (with a vertical pass only): the fused first
+// conv's pre-cast input [oh][ow][4] of that type instead (launch_x_to_px4's format and values)
+hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int C, uint8_t* tmp, void* out,
+                           hipStream_t s, DType px4 = DType::F32);
 
 // Cross-block reductions (mask boxes, crop sums) meet in "sync entries" of kSyncInts ints: the
 // blocks' atomics plus a block counter; the last block writes the result and restores the idle

@@ -13,6 +13,7 @@
 #include "unet_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace unet {
 
@@ -72,10 +73,13 @@ __global__ __launch_bounds__(256) void resample_h_kernel(const uint8_t* __restri
 
 // Vertical pass fused with the final conversion: out[c][yy][xx] = clip8(...) / 255 (fp32, the
 // reference's np.float32 division), gray (C = 1) replicated to 3 planes as convert("RGB").
-template <int C, int S>
+// TO = _Float16 / __bf16 (the photo graph on the 16-bit plans): the same fp32 values cast to TO as
+// the fused first conv's pre-cast input [oh][ow][4] (x_to_px4_kernel's format and casts), so the
+// forward skips that launch and the fp32 planes are never written.
+template <int C, int S, typename TO = float>
 __global__ __launch_bounds__(256) void resample_v_kernel(const uint8_t* __restrict__ src, int src_stride,
                                                         const int* __restrict__ bounds, const int* __restrict__ kk,
-                                                        int ksize, int oh, int ow, float* __restrict__ out) {
+                                                        int ksize, int oh, int ow, TO* __restrict__ out) {
   const int xx = blockIdx.x * 256 + threadIdx.x;
   const int yy = blockIdx.y;
   if (xx >= ow || yy >= oh) return;
@@ -101,8 +105,17 @@ __global__ __launch_bounds__(256) void resample_v_kernel(const uint8_t* __restri
       for (int c = 0; c < C; ++c) acc[c] += px[j][c] * w[j];
   }
   const size_t plane = (size_t)oh * ow, o = (size_t)yy * ow + xx;
+  if constexpr (sizeof(TO) == 2) {
+    typedef TO t4 __attribute__((ext_vector_type(4)));
+    t4 v;
 #pragma unroll
-  for (int c = 0; c < 3; ++c) out[c * plane + o] = (float)clip8_fixed(acc[C == 3 ? c : 0]) / 255.0f;
+    for (int c = 0; c < 3; ++c) v[c] = (TO)((float)clip8_fixed(acc[C == 3 ? c : 0]) / 255.0f);
+    v[3] = (TO)0.f;
+    reinterpret_cast<t4*>(out)[o] = v;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[c * plane + o] = (float)clip8_fixed(acc[C == 3 ? c : 0]) / 255.0f;
+  }
 }
 
 // No vertical resampling (ih == oh): convert the (horizontally resampled or original) rows.
@@ -116,10 +129,12 @@ __global__ __launch_bounds__(256) void to_planar_f32_kernel(const uint8_t* __res
   for (int c = 0; c < 3; ++c) out[c * plane + o] = (float)p[C == 3 ? c : 0] / 255.0f;
 }
 
-// channels: 1 (L), 3 (RGB) or 4 (RGBX: 3 channels, 4 bytes per pixel)
-hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int channels, uint8_t* tmp, float* out,
-                           hipStream_t s) {
+// channels: 1 (L), 3 (RGB) or 4 (RGBX: 3 channels, 4 bytes per pixel).  px4 != F32 (only with a
+// vertical pass): out is the pre-cast [oh][ow][4] input of that element type instead of fp32 planes.
+hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int channels, uint8_t* tmp, void* out,
+                           hipStream_t s, DType px4) {
   if ((channels != 1 && channels != 3 && channels != 4) || p.oh <= 0 || p.ow <= 0) return hipErrorInvalidValue;
+  if (px4 != DType::F32 && (!p.need_v || (px4 != DType::F16 && px4 != DType::BF16))) return hipErrorInvalidValue;
   const int C = channels == 1 ? 1 : 3, S = channels;
   const uint8_t* src = img;
   int stride = p.iw * S, sstep = S;
@@ -139,17 +154,27 @@ hipError_t launch_resample(const ResamplePlan& p, const uint8_t* img, int channe
     sstep = C;
   }
   const dim3 grid((unsigned)((p.ow + 255) / 256), (unsigned)p.oh);
-  if (p.need_v && sstep == 4)
-    hipLaunchKernelGGL((resample_v_kernel<3, 4>), grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize,
-                       p.oh, p.ow, out);
-  else if (p.need_v && sstep == 3)
-    hipLaunchKernelGGL((resample_v_kernel<3, 3>), grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize,
-                       p.oh, p.ow, out);
+  auto vpass = [&](auto* o) {
+    using TO = std::remove_pointer_t<decltype(o)>;
+    if (sstep == 4)
+      hipLaunchKernelGGL((resample_v_kernel<3, 4, TO>), grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk,
+                         p.v_ksize, p.oh, p.ow, o);
+    else if (sstep == 3)
+      hipLaunchKernelGGL((resample_v_kernel<3, 3, TO>), grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk,
+                         p.v_ksize, p.oh, p.ow, o);
+    else
+      hipLaunchKernelGGL((resample_v_kernel<1, 1, TO>), grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk,
+                         p.v_ksize, p.oh, p.ow, o);
+  };
+  if (px4 == DType::F16)
+    vpass(static_cast<_Float16*>(out));
+  else if (px4 == DType::BF16)
+    vpass(static_cast<__bf16*>(out));
   else if (p.need_v)
-    hipLaunchKernelGGL((resample_v_kernel<1, 1>), grid, dim3(256), 0, s, src, stride, p.v_bounds, p.v_kk, p.v_ksize,
-                       p.oh, p.ow, out);
+    vpass(static_cast<float*>(out));
   else
-    hipLaunchKernelGGL(to_planar_f32_kernel, grid, dim3(256), 0, s, src, stride, C, sstep, p.oh, p.ow, out);
+    hipLaunchKernelGGL(to_planar_f32_kernel, grid, dim3(256), 0, s, src, stride, C, sstep, p.oh, p.ow,
+                       static_cast<float*>(out));
   return hipGetLastError();
 }
 
