@@ -91,6 +91,23 @@ def main():
                     for j, name in enumerate(["cached_model", "lock+no_grad+stream", "stage_photo", "graph lookup+launch",
                                               "synchronize", "masks+rects copies", "crops"]):
                         secs.setdefault(name, []).append(t[j + 1] - t[j])
+            # the masks out of the pinned buffer right after the graph's DMA wrote it (cold): numpy's
+            # single-threaded copy against torch's parallel CPU copy into a fresh array
+            cold = {"numpy": [], "torch": []}
+            for it in range(2 * args.calls + 6):
+                g_.launch(stream_.cuda_stream)
+                stream_.synchronize()
+                how = "numpy" if it % 2 == 0 else "torch"
+                t0 = time.perf_counter()
+                if how == "numpy":
+                    mm = st_.hm.numpy()[0].view(np.bool_).copy()
+                else:
+                    mm = np.empty(st_.hm.shape[1:], dtype=np.bool_)
+                    torch.from_numpy(mm.view(np.uint8)).copy_(st_.hm[0])
+                cold[how].append(time.perf_counter() - t0)
+                assert mm.shape == (3, 512, 512)
+            print(f"[{dtype}] cold mask copy (median us): " +
+                  ", ".join(f"{k} {1e6 * float(np.median(v[3:])):.1f}" for k, v in cold.items()), flush=True)
             print(f"[{dtype}] run_unet sections (median us): " +
                   ", ".join(f"{k} {1e6 * float(np.median(v)):.1f}" for k, v in secs.items()), flush=True)
 
