@@ -184,3 +184,24 @@ def test_copy_rgbx_equals_the_photo_pixels():
     huge = np.empty(4032 * 3024 * 4, np.uint8)
     shape = inf.copy_rgbx(big, huge.ctypes.data, huge.size)
     assert shape is None or shape == (3024, 4032, 4)
+
+
+def test_staging_outputs_are_one_block_in_copy_order():
+    """run_unet's output buffers are carved from one block, masks | boxes | rects | sums, so the photo
+    graph copies the three small ones back as one (unet_photo_graph_create merges adjacent copies):
+    each view contiguous, of the right dtype and shape, int64 sums 8-byte aligned, no gaps."""
+    from unet_mi355x import inference as inf
+    block = torch.empty(inf._Staging._out_bytes(), dtype=torch.uint8)
+    m, b, r, s = inf._Staging._outputs(block)
+    n = len(inf.FIELDS)
+    assert m.shape == (1, n, 512, 512) and m.dtype == torch.uint8
+    assert b.shape == (1, n, 4) and b.dtype == torch.int32
+    assert r.shape == (n, 4) and r.dtype == torch.int32
+    assert s.shape == (n,) and s.dtype == torch.int64
+    base = block.data_ptr()
+    ends = base
+    for t in (m, b, r, s):
+        assert t.is_contiguous() and t.data_ptr() == ends
+        ends += t.numel() * t.element_size()
+    assert ends == base + block.numel()
+    assert (s.data_ptr() - base) % 8 == 0
