@@ -61,7 +61,9 @@ def main():
         for c, m, h in handles:
             res[c].append(h.forward_timed(x, None, masks, native.MASK_BITS, stream))
     med = {c: np.median(np.array(v), axis=0) for c, v in res.items()}
-    print(f"{'launch':14s}" + "".join(f"{c[:22]:>24s}" for c in a.cands))
+    for k, c in enumerate(a.cands):   # the columns' legend (candidates often share a long prefix)
+        print(f"c{k}: {c!r}")
+    print(f"{'launch':14s}" + "".join(f"{'c' + str(k):>24s}" for k in range(len(a.cands))))
     for i, e in enumerate(LAUNCHES):
         f = launch_flops(e, a.batch, a.size, a.size, 3) / 1e9
         print(f"{e[0]:14s}" + "".join(f"{med[c][i]:10.3f}ms {f / med[c][i]:8.0f}TF " for c in a.cands))

@@ -132,7 +132,8 @@ struct unet_handle {
   unsigned long long generation = 1;   // bumped whenever device pointers a graph captured change
   // split-K of under-filled layers (small batches, layer_split): the largest slice count
   // (UNET_MI355X_KSPLIT; 0 or 1 = never split) and per-launch forced counts for A/B runs
-  // (UNET_MI355X_KSPLIT_FORCE="i:ks,...", i = 3x3 layer 0..16 or 17 + ConvTranspose 0..3; 0 = auto)
+  // (UNET_MI355X_KSPLIT_FORCE="i:ks,...", i = 3x3 layer 0..16 or 17 + ConvTranspose 0..3; 0 = auto;
+  // ks + 100 = ks slices on 64-row tiles of the 8-wave ring)
   int ksplit_max = 32;
   int ksplit_force[21] = {};
   void* part = nullptr;   // the current forward's partial buffer (workspace region Buffers::part)
@@ -267,8 +268,10 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
     if (rows == 0) break;
     const double rate = ring8 ? (rows == 128 ? 6e12 : 4.8e12) : 0.5e12;
     const long long blocks = tiles * (L.ctot / rows);
-    if (forced > 0) {   // A/B runs: the forced slice count on the layer's own row tile
-      if (rows == own && forced <= nch && nch % forced == 0 && blocks * forced <= 8LL * cap) best = {forced, 0};
+    if (forced > 0) {   // A/B runs: ks on the layer's own row tile, ks + 100 on 64-row tiles (the ring)
+      const int fks = forced % 100, frows = forced >= 100 ? 64 : own;
+      if (rows == frows && fks <= nch && nch % fks == 0 && blocks * fks <= 8LL * cap)
+        best = {fks, rows == own ? 0 : rows};
       continue;
     }
     if (rows != own && epi != EPI_UPSCATTER) {   // finer row tiles alone, no K split (no partials)
