@@ -34,7 +34,17 @@ TD = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
 
 
 def plan_of(name: str) -> dict:
-    """layer -> storage dtype of its weights and of its INPUT operand (what its MFMA reads)."""
+    """layer -> storage dtype of its weights and of its INPUT operand (what its MFMA reads).
+    "base+layer=dt,layer=dt": a named plan with per-layer overrides (e.g. "lv01+down1.0=bf16")."""
+    if "+" in name:
+        base, _, ov = name.partition("+")
+        p = plan_of(base)
+        for item in ov.split(","):
+            k, _, dt = item.partition("=")
+            if k not in p or dt not in TD:
+                raise ValueError(item)
+            p[k] = dt
+        return p
     p = {k: "bf16" for k in LAYERS}
     if name == "fp16":
         p = {k: "fp16" for k in LAYERS}
