@@ -1219,3 +1219,33 @@ def test_doubleconv_standalone_matches_reference_hooks(dtype):
             print(f"{dtype} {name}: {tuple(xin.shape)} -> rel err {err:.3e}")
             assert got.shape == ref.shape and err <= TOL[dtype], (name, err)
     m.close()
+
+
+def test_run_unet_masks_survive_later_calls():
+    """run_unet hands out its masks as views of pinned mask blocks (no host copy); a block is reused only
+    once no returned mask of it is alive, and with every block held the call falls back to copying.  So
+    masks kept across many later calls (more than the pool holds) never change, and dropped ones free
+    their block for the next call."""
+    from unet_mi355x import inference as inf
+    photos = _photos(3)
+    with tempfile.TemporaryDirectory() as td:
+        ck = _save_ckpt(td)
+        inf.DEVICE = DEV
+        kept = []
+        for i in range(inf._Staging.MASK_POOL + 3):   # the first calls hold every block, then fall back
+            masks, _ = inf.run_unet(photos[i % 3], ck, compute_dtype="mixed")
+            kept.append((i % 3, masks, {k: v.copy() for k, v in masks.items()}))
+        for _ in range(3):                           # more calls while all of those are alive
+            inf.run_unet(photos[1], ck, compute_dtype="mixed")
+        for j, masks, snap in kept:
+            for k in inf.FIELDS:
+                assert masks[k].dtype == np.bool_ and masks[k].shape == (512, 512)
+                assert np.array_equal(masks[k], snap[k]), (j, k)
+            again, _ = inf.run_unet(photos[j], ck, compute_dtype="mixed")
+            for k in inf.FIELDS:
+                assert np.array_equal(again[k], snap[k]), (j, k)
+        st = inf._staging[str(inf.DEVICE)]
+        assert len(st.mask_blocks) == inf._Staging.MASK_POOL
+        del kept, masks, again
+        blk = st.mask_block()
+        assert blk is not None   # every returned mask dropped: a block is free again
