@@ -330,7 +330,7 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
         st = _staging.get(str(DEVICE))
         if st is None:
             st = _staging[str(DEVICE)] = _Staging(DEVICE)
-    with st.lock, torch.no_grad():
+    with st.lock:
         stream = torch.cuda.current_stream(st.device)
         if pil_img.mode in ("RGB", "L"):
             # inference.py:63-64 (Pillow-exact BICUBIC resize + convert("RGB") + /255), the forward with the
@@ -353,7 +353,8 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
             return masks, {k: crop_from_stats(pil_img, rects[i], sums[i], ch) for i, k in enumerate(FIELDS)}
         # other PIL modes (RGBA premultiplied resize, P nearest, ...): the reference's host path
         x = preprocess(pil_img.resize((IMG_SIZE, IMG_SIZE)))      # inference.py:63-64
-        model.forward_boxes(x, masks="u8", out=(st.m, st.b))
+        with torch.no_grad():
+            model.forward_boxes(x, masks="u8", out=(st.m, st.b))
         st.hm.copy_(st.m, non_blocking=True)
         st.hb.copy_(st.b, non_blocking=True)
         stream.synchronize()
