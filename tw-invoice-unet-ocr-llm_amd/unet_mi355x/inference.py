@@ -379,25 +379,40 @@ def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = N
     pil_imgs = list(pil_imgs)
     if not pil_imgs:
         return []
-    x = torch.empty((len(pil_imgs), 3, IMG_SIZE, IMG_SIZE), dtype=torch.float32, device=DEVICE)
+    n = len(pil_imgs)
+    x = torch.empty((n, 3, IMG_SIZE, IMG_SIZE), dtype=torch.float32, device=DEVICE)
+    on_dev = str(DEVICE).startswith("cuda")
+    imgs = [None] * n   # the device photos (RGB / L): crop statistics on the device, as run_unet
     for i, pil in enumerate(pil_imgs):
-        if pil.mode in ("RGB", "L") and str(DEVICE).startswith("cuda"):
-            img = torch.from_numpy(np.array(pil)).to(DEVICE)
-            model.preprocess(img, IMG_SIZE, out=x[i])
+        if pil.mode in ("RGB", "L") and on_dev:
+            imgs[i] = torch.from_numpy(np.array(pil)).to(DEVICE)
+            model.preprocess(imgs[i], IMG_SIZE, out=x[i])
         else:
             x[i] = preprocess(pil.resize((IMG_SIZE, IMG_SIZE)))[0]
-    n = len(pil_imgs)
     limit = model.native_handle(x.device).small_batch_limit() if exact else 0
     chunk = limit if limit > 0 else n
     m = torch.empty((n, len(FIELDS), IMG_SIZE, IMG_SIZE), dtype=torch.uint8, device=x.device)
     boxes = torch.empty((n, len(FIELDS), 4), dtype=torch.int32, device=x.device)
+    rects = torch.empty((n, len(FIELDS), 4), dtype=torch.int32, device=x.device)
+    sums = torch.empty((n, len(FIELDS)), dtype=torch.int64, device=x.device)
     with torch.no_grad():
         for i in range(0, n, chunk):
             model.forward_boxes(x[i:i + chunk], masks="u8", out=(m[i:i + chunk], boxes[i:i + chunk]))
-    m = m.cpu().numpy().astype(bool)
-    boxes = boxes.cpu().numpy()
+    if any(img is not None for img in imgs):
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        for i, img in enumerate(imgs):
+            if img is not None:
+                img3 = img if img.dim() == 3 else img.unsqueeze(-1)
+                native.crop_stats(img3, boxes[i], IMG_SIZE, IMG_SIZE, CROP_PAD, rects[i], sums[i], stream)
+    m = m.cpu().numpy().view(np.bool_)   # the kernel writes 0 / 1 bytes
+    boxes, rects, sums = boxes.cpu().numpy(), rects.cpu().numpy(), sums.cpu().numpy()
     out = []
     for i, pil in enumerate(pil_imgs):
         masks = {k: m[i, j] for j, k in enumerate(FIELDS)}
-        out.append((masks, boxes_to_crops(pil, boxes[i])))
+        if imgs[i] is not None:   # the reference's crop rules on device statistics: no crop pixel read here
+            ch = 3 if imgs[i].dim() == 3 else 1
+            crops = {k: crop_from_stats(pil, rects[i, j], sums[i, j], ch) for j, k in enumerate(FIELDS)}
+        else:
+            crops = boxes_to_crops(pil, boxes[i])
+        out.append((masks, crops))
     return out
