@@ -55,6 +55,12 @@ def main():
             torch.cuda.synchronize()
             total = med(lambda: inf.run_unet(pil, ck, compute_dtype=dtype), args.calls)
             print(f"[{dtype}] run_unet median {total:.3f} ms over {args.calls} calls", flush=True)
+            # the serving call over 16 photos (exact: chunks of the small-batch limit; loose: one forward)
+            for exact in (True, False):
+                batch = [pil] * 16
+                inf.run_unet_batch(batch, ck, compute_dtype=dtype, exact=exact)
+                tb = med(lambda: inf.run_unet_batch(batch, ck, compute_dtype=dtype, exact=exact), 7)
+                print(f"[{dtype}] run_unet_batch x16 exact={exact}: {tb:.3f} ms = {tb / 16:.3f} ms per photo", flush=True)
             pr = cProfile.Profile()
             pr.enable()
             for _ in range(args.calls):

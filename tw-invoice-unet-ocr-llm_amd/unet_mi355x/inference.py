@@ -382,10 +382,27 @@ def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = N
     n = len(pil_imgs)
     x = torch.empty((n, 3, IMG_SIZE, IMG_SIZE), dtype=torch.float32, device=DEVICE)
     on_dev = str(DEVICE).startswith("cuda")
-    imgs = [None] * n   # the device photos (RGB / L): crop statistics on the device, as run_unet
+    # the RGB / L photos packed into one pinned block and uploaded with one copy (the device photos also
+    # give the crop statistics, as in run_unet); other modes take the reference's host resize
+    arrs = [photo_array(p) if p.mode in ("RGB", "L") and on_dev else None for p in pil_imgs]
+    offs, total = [], 0
+    for a_ in arrs:
+        offs.append(total)
+        total += 0 if a_ is None else -(-a_.size // 256) * 256
+    imgs = [None] * n
+    if total:
+        hbuf = torch.empty(total, dtype=torch.uint8).pin_memory()
+        hnp = hbuf.numpy()
+        for a_, o in zip(arrs, offs):
+            if a_ is not None:
+                hnp[o:o + a_.size] = a_.reshape(-1)
+        dbuf = torch.empty(total, dtype=torch.uint8, device=DEVICE)
+        dbuf.copy_(hbuf, non_blocking=True)
+        for i, (a_, o) in enumerate(zip(arrs, offs)):
+            if a_ is not None:
+                imgs[i] = dbuf[o:o + a_.size].view(a_.shape)
     for i, pil in enumerate(pil_imgs):
-        if pil.mode in ("RGB", "L") and on_dev:
-            imgs[i] = torch.from_numpy(np.array(pil)).to(DEVICE)
+        if imgs[i] is not None:
             model.preprocess(imgs[i], IMG_SIZE, out=x[i])
         else:
             x[i] = preprocess(pil.resize((IMG_SIZE, IMG_SIZE)))[0]
@@ -398,14 +415,26 @@ def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = N
     with torch.no_grad():
         for i in range(0, n, chunk):
             model.forward_boxes(x[i:i + chunk], masks="u8", out=(m[i:i + chunk], boxes[i:i + chunk]))
-    if any(img is not None for img in imgs):
-        stream = torch.cuda.current_stream(x.device).cuda_stream
+    if on_dev:
+        stream = torch.cuda.current_stream(x.device)
         for i, img in enumerate(imgs):
             if img is not None:
                 img3 = img if img.dim() == 3 else img.unsqueeze(-1)
-                native.crop_stats(img3, boxes[i], IMG_SIZE, IMG_SIZE, CROP_PAD, rects[i], sums[i], stream)
-    m = m.cpu().numpy().view(np.bool_)   # the kernel writes 0 / 1 bytes
-    boxes, rects, sums = boxes.cpu().numpy(), rects.cpu().numpy(), sums.cpu().numpy()
+                native.crop_stats(img3, boxes[i], IMG_SIZE, IMG_SIZE, CROP_PAD, rects[i], sums[i], stream.cuda_stream)
+        # the masks into a pinned block from torch's host allocator: the returned masks are views of it (it
+        # goes back to the allocator's cache once none is referenced), no pageable staging copy
+        hm = torch.empty(m.shape, dtype=torch.uint8).pin_memory()
+        hm.copy_(m, non_blocking=True)
+        small = torch.cat([boxes.view(n, -1), rects.view(n, -1), sums.view(torch.int32).view(n, -1)], 1).cpu()
+        stream.synchronize()
+        m = hm.numpy().view(np.bool_)   # the kernel writes 0 / 1 bytes
+        k4 = len(FIELDS) * 4
+        boxes = small[:, :k4].numpy().reshape(n, len(FIELDS), 4)
+        rects = small[:, k4:2 * k4].numpy().reshape(n, len(FIELDS), 4)
+        sums = np.ascontiguousarray(small[:, 2 * k4:].numpy()).view(np.int64).reshape(n, len(FIELDS))
+    else:
+        m = m.cpu().numpy().view(np.bool_)
+        boxes = boxes.cpu().numpy()
     out = []
     for i, pil in enumerate(pil_imgs):
         masks = {k: m[i, j] for j, k in enumerate(FIELDS)}
