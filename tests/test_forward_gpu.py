@@ -1127,12 +1127,14 @@ def test_run_unet_photo_graphs_equal_eager_calls(dtype):
     staging buffer (its graphs are re-captured over the new buffers) and a stale graph (the cached model's
     workspace grown by a batch call) all return what the eager device path returns, bit for bit.  The
     16-bit plans' graphs resize straight into the first conv's pre-cast input (fp16 / bf16) when the
-    photo's height is not 512; 512-high, 512-wide and 512 x 512 photos take the fp32 planes + pre-cast."""
+    photo's height is not 512; 512-high, 512-wide and 512 x 512 photos take the fp32 planes + pre-cast;
+    1 x 1 and 3 x 2 photos (one-pixel crops, rectangles clamped at every edge) too."""
     from unet_mi355x import inference as inf
     extra = _photos(7)
     photos = _photos(4) + [_photos(6)[5].resize((1800, 1400)), extra[6].resize((700, 512)),
                            extra[6].resize((512, 300)), extra[6].resize((512, 512)),
-                           extra[6].convert("L").resize((333, 512))]
+                           extra[6].convert("L").resize((333, 512)),
+                           extra[6].resize((1, 1)), extra[6].convert("L").resize((3, 2))]   # tiny photos
     with tempfile.TemporaryDirectory() as td:
         ck = _save_ckpt(td)
         inf.DEVICE = DEV
