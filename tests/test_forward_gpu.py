@@ -1251,3 +1251,25 @@ def test_run_unet_masks_survive_later_calls():
         del kept, masks, again
         blk = st.mask_block()
         assert blk is not None   # every returned mask dropped: a block is free again
+
+
+def test_run_unet_batch_loose_chunks_equal_one_large_forward():
+    """run_unet_batch(exact=False) pipelines 16+ photos as chunks of 8 or more (every chunk above the
+    small-batch limit): its masks equal one forward over all the photos at once bit for bit (the
+    large-batch kernels' outputs do not depend on N)."""
+    from unet_mi355x import inference as inf
+    photos = _photos(17)
+    with tempfile.TemporaryDirectory() as td:
+        ck = _save_ckpt(td)
+        inf.DEVICE = DEV
+        loose = inf.run_unet_batch(photos, ck, compute_dtype="mixed", exact=False)
+        model = inf._cached_model(ck, "mixed")
+        x = torch.empty((len(photos), 3, 512, 512), dtype=torch.float32, device=DEV)
+        for i, p in enumerate(photos):
+            model.preprocess(torch.from_numpy(np.array(p)).to(DEV), 512, out=x[i])
+        with torch.no_grad():
+            m, _ = model.forward_boxes(x, masks="u8")
+        m = m.cpu().numpy().astype(bool)
+    for i, (masks, _) in enumerate(loose):
+        for j, k in enumerate(inf.FIELDS):
+            assert np.array_equal(masks[k], m[i, j]), (i, k)

@@ -374,74 +374,105 @@ def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = N
     photo's masks and crops are exactly run_unet's.  exact=False: one forward over the whole batch
     (the large-batch kernels: higher throughput; above the limit the logits agree with run_unet's
     within the fp32-accumulation tolerance only, so a mask pixel within rounding of its threshold
-    may differ)."""
+    may differ); it runs as chunks of 8 or more photos (each above the limit, so the outputs are those
+    of one forward over all of them).
+
+    The chunks form a pipeline on the caller's stream: while the GPU runs chunk k (upload, resize,
+    forward, crop statistics, copies back), the host packs chunk k + 1's photos and then builds chunk
+    k - 1's crops."""
     model = _cached_model(checkpoint_path, compute_dtype)
     pil_imgs = list(pil_imgs)
     if not pil_imgs:
         return []
     n = len(pil_imgs)
-    x = torch.empty((n, 3, IMG_SIZE, IMG_SIZE), dtype=torch.float32, device=DEVICE)
     on_dev = str(DEVICE).startswith("cuda")
-    # the RGB / L photos packed into one pinned block and uploaded with one copy (the device photos also
-    # give the crop statistics, as in run_unet); other modes take the reference's host resize
-    arrs = [photo_array(p) if p.mode in ("RGB", "L") and on_dev else None for p in pil_imgs]
-    offs, total = [], 0
-    for a_ in arrs:
-        offs.append(total)
-        total += 0 if a_ is None else -(-a_.size // 256) * 256
-    imgs = [None] * n
-    if total:
-        hbuf = torch.empty(total, dtype=torch.uint8).pin_memory()
-        hnp = hbuf.numpy()
-        for a_, o in zip(arrs, offs):
-            if a_ is not None:
-                hnp[o:o + a_.size] = a_.reshape(-1)
-        dbuf = torch.empty(total, dtype=torch.uint8, device=DEVICE)
-        dbuf.copy_(hbuf, non_blocking=True)
-        for i, (a_, o) in enumerate(zip(arrs, offs)):
-            if a_ is not None:
-                imgs[i] = dbuf[o:o + a_.size].view(a_.shape)
-    for i, pil in enumerate(pil_imgs):
-        if imgs[i] is not None:
-            model.preprocess(imgs[i], IMG_SIZE, out=x[i])
-        else:
-            x[i] = preprocess(pil.resize((IMG_SIZE, IMG_SIZE)))[0]
-    limit = model.native_handle(x.device).small_batch_limit() if exact else 0
-    chunk = limit if limit > 0 else n
-    m = torch.empty((n, len(FIELDS), IMG_SIZE, IMG_SIZE), dtype=torch.uint8, device=x.device)
-    boxes = torch.empty((n, len(FIELDS), 4), dtype=torch.int32, device=x.device)
-    rects = torch.empty((n, len(FIELDS), 4), dtype=torch.int32, device=x.device)
-    sums = torch.empty((n, len(FIELDS)), dtype=torch.int64, device=x.device)
-    with torch.no_grad():
-        for i in range(0, n, chunk):
-            model.forward_boxes(x[i:i + chunk], masks="u8", out=(m[i:i + chunk], boxes[i:i + chunk]))
-    if on_dev:
-        stream = torch.cuda.current_stream(x.device)
-        for i, img in enumerate(imgs):
+    if not on_dev:
+        raise RuntimeError("unet_mi355x: run_unet_batch runs on a ROCm GPU; there is no CPU fallback")
+    nf = len(FIELDS)
+    x = torch.empty((n, 3, IMG_SIZE, IMG_SIZE), dtype=torch.float32, device=DEVICE)
+    m = torch.empty((n, nf, IMG_SIZE, IMG_SIZE), dtype=torch.uint8, device=x.device)
+    boxes = torch.empty((n, nf, 4), dtype=torch.int32, device=x.device)
+    rects = torch.empty((n, nf, 4), dtype=torch.int32, device=x.device)
+    sums = torch.empty((n, nf), dtype=torch.int64, device=x.device)
+    # the masks come back into one pinned block from torch's host allocator; the returned masks are views
+    # of it (it goes back to the allocator's cache once none is referenced): no pageable staging copy
+    hm = torch.empty(m.shape, dtype=torch.uint8).pin_memory()
+    hsmall = torch.empty((n, 2 * nf * 4 + 2 * nf), dtype=torch.int32).pin_memory()   # boxes | rects | sums
+    limit = model.native_handle(x.device).small_batch_limit()
+    if exact:   # chunks of at most the limit: bitwise the batch-1 outputs
+        bounds = list(range(0, n, limit if limit > 0 else n)) + [n]
+    else:       # chunks of 8 or more photos, all above the limit: the same outputs as one large forward
+        k = max(1, n // 8) if n >= 16 else 1
+        bounds = [i * n // k for i in range(k + 1)]
+    stream = torch.cuda.current_stream(x.device)
+    out = [None] * n
+    keep = []   # the chunks' pinned photo blocks, alive until their uploads are done
+
+    def launch(lo, hi):
+        """Upload + resize + forward + crop statistics + copies back of photos lo .. hi-1 (asynchronous)."""
+        arrs = [photo_array(p) if p.mode in ("RGB", "L") else None for p in pil_imgs[lo:hi]]
+        offs, total = [], 0
+        for a_ in arrs:
+            offs.append(total)
+            total += 0 if a_ is None else -(-a_.size // 256) * 256
+        imgs = [None] * (hi - lo)
+        if total:   # the RGB / L photos packed into one pinned block, one copy
+            hbuf = torch.empty(total, dtype=torch.uint8).pin_memory()
+            hnp = hbuf.numpy()
+            for a_, o in zip(arrs, offs):
+                if a_ is not None:
+                    hnp[o:o + a_.size] = a_.reshape(-1)
+            dbuf = torch.empty(total, dtype=torch.uint8, device=x.device)
+            dbuf.copy_(hbuf, non_blocking=True)
+            keep.append(hbuf)
+            for j, (a_, o) in enumerate(zip(arrs, offs)):
+                if a_ is not None:
+                    imgs[j] = dbuf[o:o + a_.size].view(a_.shape)
+        for j in range(hi - lo):
+            if imgs[j] is not None:
+                model.preprocess(imgs[j], IMG_SIZE, out=x[lo + j])
+            else:   # other PIL modes (RGBA premultiplied resize, P nearest, ...): the reference's host resize
+                x[lo + j] = preprocess(pil_imgs[lo + j].resize((IMG_SIZE, IMG_SIZE)))[0]
+        with torch.no_grad():
+            model.forward_boxes(x[lo:hi], masks="u8", out=(m[lo:hi], boxes[lo:hi]))
+        for j, img in enumerate(imgs):
             if img is not None:
                 img3 = img if img.dim() == 3 else img.unsqueeze(-1)
-                native.crop_stats(img3, boxes[i], IMG_SIZE, IMG_SIZE, CROP_PAD, rects[i], sums[i], stream.cuda_stream)
-        # the masks into a pinned block from torch's host allocator: the returned masks are views of it (it
-        # goes back to the allocator's cache once none is referenced), no pageable staging copy
-        hm = torch.empty(m.shape, dtype=torch.uint8).pin_memory()
-        hm.copy_(m, non_blocking=True)
-        small = torch.cat([boxes.view(n, -1), rects.view(n, -1), sums.view(torch.int32).view(n, -1)], 1).cpu()
-        stream.synchronize()
-        m = hm.numpy().view(np.bool_)   # the kernel writes 0 / 1 bytes
-        k4 = len(FIELDS) * 4
-        boxes = small[:, :k4].numpy().reshape(n, len(FIELDS), 4)
-        rects = small[:, k4:2 * k4].numpy().reshape(n, len(FIELDS), 4)
-        sums = np.ascontiguousarray(small[:, 2 * k4:].numpy()).view(np.int64).reshape(n, len(FIELDS))
-    else:
-        m = m.cpu().numpy().view(np.bool_)
-        boxes = boxes.cpu().numpy()
-    out = []
-    for i, pil in enumerate(pil_imgs):
-        masks = {k: m[i, j] for j, k in enumerate(FIELDS)}
-        if imgs[i] is not None:   # the reference's crop rules on device statistics: no crop pixel read here
-            ch = 3 if imgs[i].dim() == 3 else 1
-            crops = {k: crop_from_stats(pil, rects[i, j], sums[i, j], ch) for j, k in enumerate(FIELDS)}
-        else:
-            crops = boxes_to_crops(pil, boxes[i])
-        out.append((masks, crops))
+                native.crop_stats(img3, boxes[lo + j], IMG_SIZE, IMG_SIZE, CROP_PAD, rects[lo + j], sums[lo + j],
+                                  stream.cuda_stream)
+        hm[lo:hi].copy_(m[lo:hi], non_blocking=True)
+        small = torch.cat([boxes[lo:hi].view(hi - lo, -1), rects[lo:hi].view(hi - lo, -1),
+                           sums[lo:hi].view(torch.int32).view(hi - lo, -1)], 1)
+        hsmall[lo:hi].copy_(small, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev, [img is not None for img in imgs], [None if img is None else img.dim() for img in imgs]
+
+    def finish(lo, hi, ev, dev_photo, dims):
+        """Masks (views of the pinned block) and crops of photos lo .. hi-1, once their copies landed."""
+        ev.synchronize()
+        mb = hm.numpy().view(np.bool_)   # the kernel writes 0 / 1 bytes
+        sm = hsmall.numpy()
+        k4 = nf * 4
+        for j in range(hi - lo):
+            i = lo + j
+            masks = {k: mb[i, f] for f, k in enumerate(FIELDS)}
+            bx = sm[i, :k4].reshape(nf, 4)
+            if dev_photo[j]:   # the reference's crop rules on device statistics: no crop pixel read here
+                rc = sm[i, k4:2 * k4].reshape(nf, 4)
+                sv = np.ascontiguousarray(sm[i, 2 * k4:]).view(np.int64)
+                ch = 3 if dims[j] == 3 else 1
+                crops = {k: crop_from_stats(pil_imgs[i], rc[f], sv[f], ch) for f, k in enumerate(FIELDS)}
+            else:
+                crops = boxes_to_crops(pil_imgs[i], bx)
+            out[i] = (masks, crops)
+
+    pending = None
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        cur = (lo, hi) + launch(lo, hi)
+        if pending is not None:
+            finish(*pending)
+        pending = cur
+    finish(*pending)
+    del keep
     return out
