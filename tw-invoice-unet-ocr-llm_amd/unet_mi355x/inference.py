@@ -396,7 +396,11 @@ def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = N
     sums = torch.empty((n, nf), dtype=torch.int64, device=x.device)
     # the masks come back into one pinned block from torch's host allocator; the returned masks are views
     # of it (it goes back to the allocator's cache once none is referenced): no pageable staging copy
-    hm = torch.empty(m.shape, dtype=torch.uint8).pin_memory()
+    # (pageable past 256 MB of masks -- 341 photos --: pinned memory is a scarcer resource; the copies
+    # are then synchronous)
+    hm = torch.empty(m.shape, dtype=torch.uint8)
+    if hm.numel() <= 256 << 20:
+        hm = hm.pin_memory()
     hsmall = torch.empty((n, 2 * nf * 4 + 2 * nf), dtype=torch.int32).pin_memory()   # boxes | rects | sums
     limit = model.native_handle(x.device).small_batch_limit()
     if exact:   # chunks of at most the limit: bitwise the batch-1 outputs
