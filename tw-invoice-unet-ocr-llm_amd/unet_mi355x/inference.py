@@ -215,7 +215,7 @@ class _Staging:
         # one pinned host block in the same order: the photo graph copies them back as one
         self.m, self.b, self.r, self.s = self._outputs(torch.empty(self._out_bytes(), dtype=torch.uint8,
                                                                    device=self.device))
-        self.hm, self.hb, self.hr, self.hs = self._outputs(torch.empty(self._out_bytes(), dtype=torch.uint8).pin_memory())
+        self.hm, self.hb, self.hr, self.hs = self._outputs(torch.empty(self._out_bytes(), dtype=torch.uint8, pin_memory=True))
         self.graphs: OrderedDict = OrderedDict()   # (ih, iw, c) -> (model, native.Graph)
         self.mask_blocks: list = []                # pinned [n, 512, 512] bool arrays, see mask_block
 
@@ -241,7 +241,7 @@ class _Staging:
         n = arr.size
         if self.h_img is None or self.h_img.numel() < n:
             self.drop_graphs()
-            self.h_img = torch.empty(max(n, 1 << 20), dtype=torch.uint8).pin_memory()
+            self.h_img = torch.empty(max(n, 1 << 20), dtype=torch.uint8, pin_memory=True)
             self.d_img = torch.empty(self.h_img.numel(), dtype=torch.uint8, device=self.device)
         self.h_img[:n].numpy()[:] = arr.reshape(-1)
         return self.d_img[:n].view(arr.shape)
@@ -254,7 +254,7 @@ class _Staging:
         if pil_img.mode == "RGB":
             if self.h_img is None or self.h_img.numel() < w * h * 4:
                 self.drop_graphs()
-                self.h_img = torch.empty(max(w * h * 4, 1 << 20), dtype=torch.uint8).pin_memory()
+                self.h_img = torch.empty(max(w * h * 4, 1 << 20), dtype=torch.uint8, pin_memory=True)
                 self.d_img = torch.empty(self.h_img.numel(), dtype=torch.uint8, device=self.device)
             shape = copy_rgbx(pil_img, self.h_img.data_ptr(), self.h_img.numel())
             if shape is not None:
@@ -279,7 +279,7 @@ class _Staging:
             if _refs(blk) == blk[3]:
                 return i
         if len(self.mask_blocks) < self.MASK_POOL:
-            t = torch.empty(self.m.shape[1:], dtype=torch.uint8).pin_memory()
+            t = torch.empty(self.m.shape[1:], dtype=torch.uint8, pin_memory=True)
             u = t.numpy()
             blk = [t, u.view(np.bool_), u, None]
             del u
@@ -398,10 +398,8 @@ def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = N
     # of it (it goes back to the allocator's cache once none is referenced): no pageable staging copy
     # (pageable past 256 MB of masks -- 341 photos --: pinned memory is a scarcer resource; the copies
     # are then synchronous)
-    hm = torch.empty(m.shape, dtype=torch.uint8)
-    if hm.numel() <= 256 << 20:
-        hm = hm.pin_memory()
-    hsmall = torch.empty((n, 2 * nf * 4 + 2 * nf), dtype=torch.int32).pin_memory()   # boxes | rects | sums
+    hm = torch.empty(m.shape, dtype=torch.uint8, pin_memory=m.numel() <= 256 << 20)
+    hsmall = torch.empty((n, 2 * nf * 4 + 2 * nf), dtype=torch.int32, pin_memory=True)   # boxes | rects | sums
     limit = model.native_handle(x.device).small_batch_limit()
     if exact:   # chunks of at most the limit: bitwise the batch-1 outputs
         bounds = list(range(0, n, limit if limit > 0 else n)) + [n]
@@ -421,7 +419,7 @@ def run_unet_batch(pil_imgs, checkpoint_path: str, compute_dtype: str | None = N
             total += 0 if a_ is None else -(-a_.size // 256) * 256
         imgs = [None] * (hi - lo)
         if total:   # the RGB / L photos packed into one pinned block, one copy
-            hbuf = torch.empty(total, dtype=torch.uint8).pin_memory()
+            hbuf = torch.empty(total, dtype=torch.uint8, pin_memory=True)   # (allocated pinned: no copy)
             hnp = hbuf.numpy()
             for a_, o in zip(arrs, offs):
                 if a_ is not None:
