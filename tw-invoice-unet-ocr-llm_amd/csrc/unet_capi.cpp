@@ -17,6 +17,7 @@
 #include <list>
 #include <map>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -438,9 +439,9 @@ void pack_first_mfma(DType t0, const std::vector<double>& w, int C, std::vector<
 // Ring kernels (cfg_is_ring) take the same rows in step order instead: per row tile of BR rows,
 // step s = (c / BKE) * 9 + tap holds a contiguous [BR][BKE] block (BKE = 64 bytes of K), so
 // packed[((ct * S + s) * BR + rho % BR) * BKE + c % BKE], S = 9 * cin / BKE.
-int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::vector<double>& b) {
+int pack3x3_host(const Layer& L, const std::vector<double>& w, std::vector<uint8_t>& buf) {
   const int K = 9 * L.cin;
-  std::vector<uint8_t> buf((size_t)L.cout * K * dtype_size(L.dt));
+  buf.assign((size_t)L.cout * K * dtype_size(L.dt), 0);
   const bool ring = cfg_is_ring(L.cfg);
   const int BR = cfg_rows(L.cfg), BKE = 64 / (int)dtype_size(L.dt), S = K / BKE;
   if (ring && (L.cout % BR || L.cin % BKE)) return fail(UNET_EINVAL, "ring kernel tiling does not divide the layer");
@@ -453,8 +454,13 @@ int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::v
         put_elem(L.dt, buf, idx, w[((size_t)o * L.cin + c) * 9 + tap]);
       }
   }
-  std::vector<float> bf(b.begin(), b.end());
-  int rc = upload(h, &L.w, buf.data(), buf.size());
+  return UNET_OK;
+}
+int pack3x3(unet_handle* h, Layer& L, const std::vector<double>& w, const std::vector<double>& b) {
+  std::vector<uint8_t> buf;
+  int rc = pack3x3_host(L, w, buf);
+  const std::vector<float> bf(b.begin(), b.end());
+  if (!rc) rc = upload(h, &L.w, buf.data(), buf.size());
   if (!rc) rc = upload(h, (void**)&L.b, bf.data(), bf.size() * 4);
   return rc;
 }
@@ -1004,11 +1010,37 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
       if (rc) return rc;
     }
   }
-  for (int i = 0; i < 17; ++i) {
-    rc = fold(sd, kLayerKey[i][0], kLayerKey[i][1], h->L[i].cin, h->L[i].cout, w, b);
-    if (!rc) rc = check_f16_range(h->L[i].dt, w, b, std::string(kLayerKey[i][0]) + ".net." + kLayerKey[i][1]);
-    if (!rc) rc = pack3x3(h, h->L[i], w, b);
-    if (rc) return rc;
+  {   // the 17 3x3 layers (29 M of the 31 M weights): BN fold + range check + packing on host threads,
+      // largest layers first; then the uploads in order on this thread (a cold start's ~0.1 s)
+    struct Packed { std::vector<uint8_t> w; std::vector<float> b; int rc = UNET_OK; std::string err; };
+    std::vector<Packed> pk(17);
+    std::vector<int> order(17);
+    for (int i = 0; i < 17; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int a, int c) {
+      return (long long)h->L[a].cin * h->L[a].cout > (long long)h->L[c].cin * h->L[c].cout;
+    });
+    auto job = [&](int i) {
+      std::vector<double> wl, bl;
+      Packed& P = pk[i];
+      P.rc = fold(sd, kLayerKey[i][0], kLayerKey[i][1], h->L[i].cin, h->L[i].cout, wl, bl);
+      if (!P.rc) P.rc = check_f16_range(h->L[i].dt, wl, bl, std::string(kLayerKey[i][0]) + ".net." + kLayerKey[i][1]);
+      if (!P.rc) P.rc = pack3x3_host(h->L[i], wl, P.w);
+      if (P.rc) P.err = g_err;   // the worker's own thread-local message
+      P.b.assign(bl.begin(), bl.end());
+    };
+    const int nt = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t)
+      pool.emplace_back([&, t]() { for (int k = t; k < 17; k += nt) job(order[k]); });
+    for (int k = 0; k < 17; k += nt) job(order[k]);
+    for (auto& th : pool) th.join();
+    for (int i = 0; i < 17; ++i) {
+      if (pk[i].rc) return fail(pk[i].rc, pk[i].err);
+      rc = upload(h, &h->L[i].w, pk[i].w.data(), pk[i].w.size());
+      if (!rc) rc = upload(h, (void**)&h->L[i].b, pk[i].b.data(), pk[i].b.size() * 4);
+      if (rc) return rc;
+      std::vector<uint8_t>().swap(pk[i].w);
+    }
   }
   std::string err;
   for (int i = 0; i < 4; ++i) {

@@ -42,11 +42,18 @@ _cache_lock = threading.Lock()
 
 
 def load_model(checkpoint_path: str, compute_dtype: str | None = None):
-    """inference.py:17-24: UNet(3,3) on DEVICE, strict state_dict load, eval()."""
-    model = UNet(n_channels=3, n_classes=3, compute_dtype=compute_dtype, thresholds=THRESHOLDS).to(DEVICE)
-    state = torch.load(checkpoint_path, map_location=DEVICE, weights_only=True)
-    model.load_state_dict(state)
+    """inference.py:17-24: UNet(3,3) on DEVICE, strict state_dict load, eval().  The module is built on
+    DEVICE (its random initialisation runs there, not as 31 M host draws; the meta device would cost
+    ~0.7 s of one-time setup in a fresh process) and takes the checkpoint's tensors (strict,
+    assign=True), and the native handle is packed from the host copies the checkpoint was read into (no
+    read-back of the weights from the device): the cold start of the first run_unet."""
+    state = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+    with torch.device(DEVICE):
+        model = UNet(n_channels=3, n_classes=3, compute_dtype=compute_dtype, thresholds=THRESHOLDS)
+    model.load_state_dict({k: v.to(DEVICE) for k, v in state.items()}, assign=True)
     model.eval()
+    if str(DEVICE).startswith("cuda"):
+        model._prepack(torch.device(DEVICE), state)
     return model
 
 

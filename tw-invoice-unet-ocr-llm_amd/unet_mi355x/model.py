@@ -204,6 +204,19 @@ class UNet(nn.Module):
                 self._packed_sig[idx] = sig
         return h
 
+    def _prepack(self, device: torch.device, host_state) -> None:
+        """Pack the native handle for ``device`` from ``host_state``: host copies of exactly the module's
+        current weights (inference.load_model passes the checkpoint it just assigned), so the pack reads
+        no weight back from the device.  The handle then counts as packed for the current weights."""
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        with self._lock:
+            h = self._handles.get(idx)
+            if h is None:
+                h = native.Handle(self.n_channels, self.n_classes, self.compute_dtype, idx, self.thresholds)
+                self._handles[idx] = h
+            h.load_weights(host_state)
+            self._packed_sig[idx] = self._signature()
+
     def _check_input(self, x: torch.Tensor):
         if not isinstance(x, torch.Tensor) or x.dim() != 4:
             raise RuntimeError("UNet.forward expects a 4-D NCHW tensor")
