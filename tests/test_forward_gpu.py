@@ -1273,3 +1273,33 @@ def test_run_unet_batch_loose_chunks_equal_one_large_forward():
     for i, (masks, _) in enumerate(loose):
         for j, k in enumerate(inf.FIELDS):
             assert np.array_equal(masks[k], m[i, j]), (i, k)
+
+
+def test_run_unet_from_several_threads():
+    """A Streamlit server may call run_unet from several session threads at once: the calls serialise on
+    the device's staging lock and every thread gets exactly the single-threaded result for its photo
+    (photo graphs, mask blocks and the cached model are shared state)."""
+    import threading
+    from unet_mi355x import inference as inf
+    photos = _photos(4)
+    with tempfile.TemporaryDirectory() as td:
+        ck = _save_ckpt(td)
+        inf.DEVICE = DEV
+        want = [inf.run_unet(p, ck, compute_dtype="mixed") for p in photos]
+        errors = []
+
+        def worker(t):
+            try:
+                for r in range(6):
+                    i = (t + r) % len(photos)
+                    _same_result(inf.run_unet(photos[i], ck, compute_dtype="mixed"), want[i], inf.FIELDS)
+            except Exception as e:   # noqa: BLE001 - reported below
+                errors.append(repr(e))
+
+        threads = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join(120)
+        assert not any(th.is_alive() for th in threads)
+        assert errors == []
