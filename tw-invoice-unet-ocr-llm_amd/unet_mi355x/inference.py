@@ -207,8 +207,9 @@ def _refs(blk):
 class _Staging:
     """Buffers of one device's run_unet calls, reused across calls: the photo (pinned host + device),
     the network input, the u8 masks and boxes, the crop statistics (device + pinned host), so a call
-    allocates nothing and makes ONE stream synchronisation; and the photo graphs captured over them
-    (one per (model, photo geometry), LRU-bounded), which stay valid while these buffers do."""
+    allocates nothing and makes ONE stream synchronisation; the pinned mask blocks run_unet returns its
+    masks in (mask_block); and the photo graphs captured over them (one per photo geometry and mask
+    block, of one model, LRU-bounded), which stay valid while these buffers do."""
 
     MASK_POOL = 4   # pinned mask blocks handed out as run_unet's masks (no host copy), see mask_block
     MAX_GRAPHS = 2 * (MASK_POOL + 1)   # a geometry's graphs: one per mask block + the copying one
@@ -223,7 +224,7 @@ class _Staging:
         self.m, self.b, self.r, self.s = self._outputs(torch.empty(self._out_bytes(), dtype=torch.uint8,
                                                                    device=self.device))
         self.hm, self.hb, self.hr, self.hs = self._outputs(torch.empty(self._out_bytes(), dtype=torch.uint8, pin_memory=True))
-        self.graphs: OrderedDict = OrderedDict()   # (ih, iw, c) -> (model, native.Graph)
+        self.graphs: OrderedDict = OrderedDict()   # ((ih, iw, c), block) -> (model, native.Graph)
         self.mask_blocks: list = []                # pinned [n, 512, 512] bool arrays, see mask_block
 
     @staticmethod
