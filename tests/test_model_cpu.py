@@ -205,3 +205,28 @@ def test_staging_outputs_are_one_block_in_copy_order():
         ends += t.numel() * t.element_size()
     assert ends == base + block.numel()
     assert (s.data_ptr() - base) % 8 == 0
+
+
+def test_mask_blocks_are_reused_only_when_unreferenced(monkeypatch):
+    """run_unet's pinned mask blocks (inference._Staging.mask_block): a block is handed out again only
+    once no mask returned in it is referenced (the masks are views of it), a fifth concurrent holder
+    gets -1 (the copying path).  CPU stand-in: pinned allocation replaced by a plain one."""
+    from unet_mi355x import inference as inf
+    real_empty = torch.empty
+    monkeypatch.setattr(torch, "empty", lambda *a, **k: real_empty(*a, **{x: v for x, v in k.items() if x != "pin_memory"}))
+    st = inf._Staging.__new__(inf._Staging)
+    st.m = real_empty((1, 3, 8, 8), dtype=torch.uint8)
+    st.mask_blocks = []
+    i0 = st.mask_block()
+    assert i0 == 0 and st.mask_block() == 0           # idle: the same block again
+    held = {k: st.mask_blocks[0][1][j] for j, k in enumerate(inf.FIELDS)}
+    assert st.mask_block() == 1                       # block 0 is held by the masks' views
+    one = held["date"]
+    del held
+    assert st.mask_block() == 1                       # one field kept: block 0 still held
+    del one
+    assert st.mask_block() == 0                       # all dropped: block 0 free again
+    keep = [st.mask_blocks[st.mask_block()][1][0] for _ in range(inf._Staging.MASK_POOL)]
+    assert st.mask_block() == -1                      # every block held: the copying graph
+    del keep
+    assert st.mask_block() == 0
