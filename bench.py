@@ -349,10 +349,25 @@ def make_leg(runner, rank, world, n_total, per_rank, seed, S, C, dev, chunk, col
     return {"x": x, "gather": gather, "step": step, "n_total": n_total, "n_local": n_local}
 
 
+class HostMark:
+    """torch.cuda.Event's record / elapsed_time on the host clock: the CPU stand-in's per-step marks."""
+
+    def __init__(self):
+        self.t = None
+
+    def record(self):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return 1e3 * (other.t - self.t)
+
+
 def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
     """The bench contract's timing loop (udist.timed_steps): barrier + sync on both sides, the MAX
-    over ranks; optional per-step GPU times (HIP events on this stream) as a diagnostic, and -- when
-    the leg's step runs the collective -- the all-gather's own time per step (events around it)."""
+    over ranks; optional per-step GPU times (HIP events on this stream; host marks for the CPU
+    stand-in) as a diagnostic, and -- when the leg's step runs the collective -- the all-gather's own
+    time per step (marks around it) and this rank's compute time per step (step start to the
+    all-gather: its forwards)."""
     # no Python garbage collection inside the timed steps (timeit's practice): a collection pass over
     # torch's and numpy's objects pauses the launching thread for milliseconds, and the GPU idles
     gc.collect()
@@ -363,9 +378,10 @@ def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
     if per_step_events:
         # created and recorded once before the warmup: torch creates the HIP events lazily at their first
         # record, which would otherwise happen inside the timed steps
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        mark = HostMark if dev.type == "cpu" else (lambda: torch.cuda.Event(enable_timing=True))
+        ev = [mark() for _ in range(steps + 1)]
         if collective:
-            ag = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+            ag = [(mark(), mark()) for _ in range(steps)]
         for e in ev + [e for pair in (ag or ()) for e in pair]:
             e.record()
     for _ in range(warmup):
@@ -394,9 +410,21 @@ def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
            "value": leg["n_total"] * steps / elapsed, "host_step_ms": [round(1e3 * t, 3) for t in host]}
     if ev:
         out["step_ms"] = [round(ev[i].elapsed_time(ev[i + 1]), 3) for i in range(steps)]
+        # this rank's forwards per step: the whole step without an exchange, else up to the all-gather
+        out["compute_ms"] = out["step_ms"] if not ag else \
+            [round(ev[i].elapsed_time(ag[i][0]), 3) for i in range(steps)]
     if ag:
         out["allgather_ms"] = [round(a.elapsed_time(b), 4) for a, b in ag]
     return out
+
+
+def over_ranks(v, dev):
+    """(max, min) of a per-rank scalar over the ranks (one all-reduce each; v itself at world 1)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return v, v
+    t = torch.tensor([v, -v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0].item()), -float(t[1].item())
 
 
 # ----------------------------------------------------------------------------- measurement legs
@@ -452,8 +480,31 @@ def kernel_table(runner, model, x, masks, B, S, C, dtype, traffic_json):
                 "launches_per_step": dom["launches"], "avg_launch_ms": dom["avg_launch_ms"],
                 "gflop_per_launch": round(dom["gflop"] / dom["launches"], 1),
                 "algo_bytes_per_launch": round(dom["algo_gb"] * 1e9 / dom["launches"])}
+    roofline.update(min_3x3(labels, ms, B, S, C, peak))
     total_gflop = sum(launch_flops(e, B, S, S, C) for e in LAUNCHES) / 1e9
     return kernels, layer_ms, roofline, total_gflop, sum(ms)
+
+
+def min_3x3(labels, ms, n, s, c_in, peak):
+    """north_star's "≥ 40 % of MFMA peak on the 3x3 DoubleConv layers" as scalars: per launch that runs a
+    3x3 layer (HIP-event time of that launch), its 3x3 FLOPs / time / peak, and the minimum over them.
+    ``min_3x3_frac`` credits a launch with every 3x3 conv it runs (down1.0 inside the fused down1.3 launch
+    of the 16-bit plans) and nothing else (the fused up1 ConvTranspose and the 1x1 head are left out);
+    ``min_3x3_frac_own`` credits it with its own layer only (down1.3 without down1.0)."""
+    fused_first = labels[0].startswith("x_to_px4")
+    best = (None, 9.0, 9.0)
+    for i, (entry, lab, t) in enumerate(zip(LAUNCHES, labels, ms)):
+        if entry[4] != "c3" or not lab or t <= 0:
+            continue
+        name, cin, cout, lvl, _ = entry
+        own = 2.0 * 9 * cin * cout * (s >> lvl) * (s >> lvl) * n
+        f = own + (launch_flops(LAUNCHES[0], n, s, s, c_in) if i == 1 and fused_first else 0.0)
+        frac, frac_own = f / (t * 1e9) / peak, own / (t * 1e9) / peak
+        if frac < best[1]:
+            best = (name, frac, frac_own)
+    if best[0] is None:
+        return {}
+    return {"min_3x3_layer": best[0], "min_3x3_frac": round(best[1], 4), "min_3x3_frac_own": round(best[2], 4)}
 
 
 def cpu_baseline(args, sd, x, masks, C, S, extra=()):
@@ -720,7 +771,10 @@ def main():
     if not args.standin and args.weights == "structured":
         runner.recentre(main_leg["x"])
         runner.handle()   # re-pack now: the legs' step functions hold this handle and never re-check weights
-    res = time_leg(main_leg, args.steps, args.warmup, sync, dev, per_step_events=not args.standin)
+    res = time_leg(main_leg, args.steps, args.warmup, sync, dev, per_step_events=True)
+    # per-rank compute (the forwards of its shard, before the exchange): MAX and MIN over the ranks, so a
+    # scaling line splits lost efficiency into compute imbalance and exchange
+    comp_max, comp_min = over_ranks(float(np.mean(res["compute_ms"])), dev)
 
     # ---- strong-scaling shapes (same timing protocol, fewer steps)
     strong_out = []
@@ -773,6 +827,7 @@ def main():
                        "parallelism": f"dp{world}", "exchange": "all_gather_into_tensor" if exchange else None,
                        "precision_plan": PLAN[args.dtype]},
             "allgather_ms": round(float(np.mean(ag)), 4) if ag else None,
+            "compute_ms": round(comp_max, 3), "compute_ms_min": round(comp_min, 3),
             "roofline": roofline, "cpu_baseline": cpu,
         }
         if out["roofline"] is not None and ag:
@@ -797,6 +852,7 @@ def main():
         out["latency_bs1"] = None if lat is None else {
             dt: {k: v for k, v in l.items() if k != "forward_bs1_layer_ms"} for dt, l in lat.items()}
         detail = {"step_ms": res.get("step_ms"), "host_step_ms": res["host_step_ms"], "allgather_ms": ag,
+                  "compute_ms": res["compute_ms"],
                   "kernels": kernels, "layer_ms": layer_ms, "fp32": fp32, "cfg5": cfg5, "latency_bs1": lat}
         line = json.dumps(out)
         print("bench_detail " + json.dumps(detail), file=sys.stderr, flush=True)

@@ -32,8 +32,9 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 4   /* 2: unet_forward requires unet_reserve; Cfg renumbered; fp16 range check. 3: unet_crop_stats.
-                                 4: unet_launch_label_at, unet_small_batch_limit, unet_photo_graph_create, unet_block_* */
+#define UNET_ABI_VERSION 5   /* 2: unet_forward requires unet_reserve; Cfg renumbered; fp16 range check. 3: unet_crop_stats.
+                                 4: unet_launch_label_at, unet_small_batch_limit, unet_photo_graph_create, unet_block_*
+                                 5: unet_photo_graph_set_masks (the masks copy is its own node) */
 
 /* error codes */
 #define UNET_OK 0
@@ -216,15 +217,21 @@ int unet_graph_destroy(unet_graph* g);
  * conv's pre-cast input into the workspace instead and x is not written; the graph owns its resize
  * tables and row buffer, so the handle's geometry cache may evict its own copy), unet_forward_boxes at N = 1 (masks / mask_kind / boxes as there), unet_crop_stats (pad,
  * rects, sums as there) and the copies of masks, boxes, rects and sums into the pinned host buffers
- * given (each may be NULL; copies whose device and host buffers both follow the previous one's in
- * memory, e.g. masks | boxes | rects | sums carved from one device and one host block, are made
- * as one) -- captured once and replayed by unet_graph_launch: one host call and one stream
- * synchronisation per photo.  Needs unet_reserve(h, 1, size, size) first; stale (UNET_ESTATE at
- * launch) under the same rules as unet_graph_create's graphs.  Destroy with unet_graph_destroy. */
+ * given (each may be NULL; the masks copy is a node of its own; of the others, copies whose device and
+ * host buffers both follow the previous one's in memory, e.g. boxes | rects | sums carved from one
+ * device and one host block, are made as one) -- captured once and replayed by unet_graph_launch: one
+ * host call and one stream synchronisation per photo.  Needs unet_reserve(h, 1, size, size) first;
+ * stale (UNET_ESTATE at launch) under the same rules as unet_graph_create's graphs.  Destroy with
+ * unet_graph_destroy. */
 int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih, int iw, int channels, float* x,
                             int size, void* masks, int mask_kind, int32_t* boxes, double pad, int32_t* rects,
                             uint64_t* sums, void* h_masks, void* h_boxes, void* h_rects, void* h_sums,
                             unet_graph** out);
+/* Retarget a photo graph's masks copy (created with h_masks != NULL) to another pinned host buffer of the
+ * same size, for its next replays (hipGraphExecMemcpyNodeSetParams1D): one graph per photo geometry serves
+ * any number of caller-held mask buffers.  Host-side only; replays already enqueued keep their target.
+ * Call it under the same serialisation as unet_graph_launch. */
+int unet_photo_graph_set_masks(unet_graph* g, void* h_masks);
 
 /* Multi-GPU data parallelism: one process per GPU, each rank runs
  * unet_forward / unet_forward_boxes on its contiguous shard of the batch, and the one exchange
@@ -248,8 +255,9 @@ int unet_destroy(unet_handle* h);
  * conv3x3 + BN + ReLU twice, padding 1) on its own, on the network's kernels: the first-conv kernel
  * for in_ch 1 or 3 (out_ch 64), the 8-wave MFMA rings (16-bit plans; MIXED = fp16 up to 128 output
  * channels, bf16 beyond, as the network's levels) or the fp32 LDS-halo kernels.  Supported: in_ch in
- * {1, 3} with out_ch 64, or in_ch a multiple of 32 with out_ch a multiple of 64 -- every block of the
- * reference UNet (UNET_ESHAPE otherwise).  Any H, W >= 1.
+ * {1, 3} with out_ch 64, or in_ch a multiple of 32 with out_ch a multiple of 64 (on the 16-bit plans:
+ * out_ch 64 or a multiple of 128, the ring tiles) -- every block of the reference UNet (UNET_ESHAPE
+ * otherwise, at unet_block_create).  Any H, W >= 1.
  * unet_block_load_weights takes the block's own 14 state_dict keys (net.0.weight, net.0.bias,
  * net.1.weight / bias / running_mean / running_var / num_batches_tracked, and net.3 / net.4 alike;
  * BN folded, eps 1e-5).  x / y: device fp32 NCHW [N][in_ch][H][W] / [N][out_ch][H][W]; the workspace

@@ -78,6 +78,37 @@ def test_torchrun_launch():
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 4
 
 
+@pytest.mark.parametrize("launcher", ["self", "torchrun"])
+def test_world_eight_ragged_strong_legs(launcher, tmp_path):
+    """The driver's N = 8 launch, both ways (bench.py spawning its 8 ranks / torch.distributed.run), with
+    the strong-scaling legs of north_star (global 256: 32 per rank) and config 4 (global 1024, chunked
+    forwards of --batch images) plus a ragged global batch (1021 = 5 x 128 + 3 x 127): the line reports
+    the MAX-over-ranks compute time beside the all-gather's, and the ragged shard sizes."""
+    detail = tmp_path / "d.json"
+    args = [BENCH, "--gpus", "8", "--batch", "32", "--strong-global", "256", "1024", "1021",
+            "--detail-out", str(detail), "--standin", "--size", "16", "--steps", "2", "--warmup", "1"]
+    if launcher == "self":
+        cmd = [sys.executable] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    p, lines = _run(cmd, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8"
+    assert out["config"]["global_batch"] == 256 and out["config"]["per_gpu_batch"] == 32
+    assert out["allgather_ms"] is not None and out["compute_ms"] is not None
+    assert 0 < out["compute_ms_min"] <= out["compute_ms"] < out["ms_per_step"] + 1e-6
+    legs = {leg["global_batch"]: leg for leg in out["strong_scaling"]}
+    assert legs[256]["per_rank_batch"] == [32] * 8
+    assert legs[1024]["per_rank_batch"] == [128] * 8
+    assert legs[1021]["per_rank_batch"] == [128] * 5 + [127] * 3
+    assert all(leg["value"] > 0 for leg in legs.values())
+    rec = json.loads(detail.read_text())
+    assert len(rec["detail"]["compute_ms"]) == 2 and len(rec["detail"]["allgather_ms"]) == 2
+
+
 def test_world_size_mismatch_fails_instead_of_benchmarking_one_gpu():
     env = _env()
     env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))

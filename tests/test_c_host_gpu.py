@@ -38,6 +38,22 @@ def write_inputs(d, sd, x, thresholds):
     np.ascontiguousarray(x, dtype=np.float32).tofile(os.path.join(d, "x.bin"))
 
 
+@pytest.fixture(scope="module", autouse=True)
+def c_host_binary():
+    """Bring the C host up to date (`make c_host`: the library's own test target, incremental: it rebuilds
+    only when the source, the header or the library changed); skip the module without a C compiler and
+    no binary."""
+    import shutil
+    if shutil.which("make") is None or shutil.which(os.environ.get("CC", "cc")) is None:
+        if not os.path.exists(BIN):
+            pytest.skip("no C compiler to build tests/c_host/unet_c_host")
+        return BIN
+    r = subprocess.run(["make", "-C", os.path.join(REPO, "tw-invoice-unet-ocr-llm_amd", "csrc"), "c_host"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return BIN
+
+
 def test_c_host_binary_matches_the_header():
     """The C host links the library and agrees with the header's ABI version (no GPU call)."""
     r = subprocess.run([BIN, "--abi"], capture_output=True, text=True, timeout=60)

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for f in declared_functions():
         assert hasattr(lib, f), f
         assert f in native.SIGNATURES, f
-    assert lib.unet_abi_version() == native.ABI_VERSION == 4
+    assert lib.unet_abi_version() == native.ABI_VERSION == 5
     assert lib.unet_last_error() is not None
 
 

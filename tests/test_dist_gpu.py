@@ -147,6 +147,99 @@ def test_two_ranks_share_one_gpu_gloo_exchange(monkeypatch):
     assert got[0][1] == got[1][1], "the MAX-over-ranks elapsed time differs between ranks"
 
 
+def _world8_rank(rank, world, port, out_dir, q):
+    """One rank of BASELINE config 4's workload on the one-GPU box: bench.py's own runner, sharding
+    (make_leg: rank r's contiguous shard of the global batch, forwards in chunks of the reserved
+    workspace) and timing loop (time_leg: barriers, per-step marks, the MAX-over-ranks all-reduce), with
+    the exchange -- all_gather_into_tensor of the bit-packed masks -- over gloo instead of RCCL."""
+    import argparse
+    import hashlib
+    sys.path.insert(0, REPO)
+    import torch.distributed as tdist
+    try:
+        import bench
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        tdist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        runner = bench.NativeRunner(argparse.Namespace(channels=3, weights="pretrained", dtype="mixed"), dev, world)
+        runner.reserve(W8_CHUNK, 512)
+        leg = bench.make_leg(runner, rank, world, W8_GLOBAL, None, W8_SEED, 512, 3, dev, W8_CHUNK)
+        t = bench.time_leg(leg, 1, 1, torch.cuda.synchronize, dev, per_step_events=True)
+        comp = bench.over_ranks(float(t["compute_ms"][0]), dev)
+        rows = leg["gather"].rows().cpu().numpy()
+        if rank == 0:
+            np.save(os.path.join(out_dir, "gathered.npy"), rows)
+        q.put((rank, (hashlib.sha256(rows.tobytes()).hexdigest(), t["elapsed"], comp, leg["n_local"],
+                      t["allgather_ms"][0])))
+        runner.model.close()
+        tdist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
+
+
+W8_GLOBAL, W8_CHUNK, W8_SEED = 1024, 32, 3000
+
+
+@pytest.mark.timeout(600)
+def test_world_eight_ranks_config4_on_one_gpu(tmp_path):
+    """BASELINE config 4 (global batch 1024 at 512^2 over 8 ranks: 128 images each) with 8 fresh rank
+    processes on cuda:0: every rank runs its shard through bench.py's make_leg / time_leg (chunked
+    forwards of 32 images, so eight workspaces fit one GPU's HBM) and all-gathers the bit-packed masks
+    over gloo.  Every rank's gathered 1024 masks equal a one-process forward of the whole batch (here in
+    forwards of 256: another batch size than the ranks') bit for bit, and the MAX-over-ranks step time
+    and compute time agree on all ranks.  Only the transport (gloo vs RCCL over xGMI) differs from the
+    8-GPU run."""
+    import socket
+    sys.path.insert(0, REPO)
+    import bench
+    from unet_mi355x import dist as udist, native
+    world = 8
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_world8_rank, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = dict(q.get(timeout=420) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert not isinstance(got[r], str), got[r]
+    assert [got[r][3] for r in range(world)] == [128] * 8
+    assert len({got[r][0] for r in range(world)}) == 1, "ranks gathered different masks"
+    assert len({got[r][1] for r in range(world)}) == 1, "the MAX-over-ranks step time differs between ranks"
+    assert len({got[r][2] for r in range(world)}) == 1, "the MAX/MIN compute times differ between ranks"
+    cmax, cmin = got[0][2]
+    assert 0 < cmin <= cmax <= 1e3 * got[0][1] + 1e-3
+    gathered = np.load(tmp_path / "gathered.npy")
+    assert gathered.shape == (W8_GLOBAL, 3, 512, 64)
+    # the one-process forward of the same global batch: rank r's pages are gen_pages(seed + r, shard)
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in bench.syn.make_state_dict(0, 3, 3, "pretrained").items()}
+    from unet_mi355x.model import UNet
+    m = UNet(3, 3, compute_dtype="mixed")
+    m.load_state_dict(sd)
+    m = m.to("cuda:0").eval()
+    pages = np.concatenate([bench.gen_pages(W8_SEED + r, 128, 512, 3) for r in range(world)])
+    h = m.native_handle(torch.device("cuda", 0))
+    h.reserve(256, 512, 512)
+    stream = torch.cuda.current_stream().cuda_stream
+    ref = torch.empty((W8_GLOBAL, 3, 512, 64), dtype=torch.uint8, device="cuda:0")
+    for i in range(0, W8_GLOBAL, 256):
+        h.forward(torch.from_numpy(pages[i:i + 256]).to("cuda:0"), None, ref[i:i + 256], native.MASK_BITS, stream)
+    ref = ref.cpu().numpy()
+    m.close()
+    assert udist.shard_bounds(W8_GLOBAL, 7, world) == (896, 1024)
+    assert np.array_equal(gathered, ref), "the 8 ranks' gathered masks differ from the one-process forward"
+
+
 _WORLD1_SCRIPT = r"""
 import os, sys, json
 import numpy as np, torch, torch.distributed as dist

@@ -872,10 +872,23 @@ def test_preprocess_geometry_cache_is_bounded():
     m.close()
 
 
-def test_run_unet_boundary_matches_reference_golden():
-    """inference.run_unet (drop-in) on the golden 600x400 photo vs the reference's masks/crops."""
+@pytest.mark.parametrize("pillow", ["current", "pillow_10_2"])
+def test_run_unet_boundary_matches_reference_golden(pillow, monkeypatch):
+    """inference.run_unet (drop-in) on the golden 600x400 photo vs the reference's masks/crops.
+    "pillow_10_2": the reference's pinned Pillow (requirements.txt:3) has no Arrow export and the raw
+    encoder is treated as unavailable too, so run_unet's photo graph takes the packed-photo path
+    (np.asarray, 3 bytes per pixel) -- same masks and crops."""
     from PIL import Image
     from unet_mi355x import inference as inf
+    if pillow == "pillow_10_2":
+        monkeypatch.setattr(inf, "copy_rgbx", lambda *a, **k: None)
+
+        def no_encoder(*a, **k):
+            raise AttributeError("_getencoder")
+        monkeypatch.setattr(inf.Image, "_getencoder", no_encoder)
+        calls = []
+        real_stage = inf._Staging.stage
+        monkeypatch.setattr(inf._Staging, "stage", lambda self, arr: calls.append(arr.shape) or real_stage(self, arr))
     z = np.load(os.path.join(GOLD, "run_unet_600x400.npz"))
     sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile="structured")
     sd["out_conv.bias"] = sd["out_conv.bias"] + z["out_bias_delta"]
@@ -886,6 +899,8 @@ def test_run_unet_boundary_matches_reference_golden():
         torch.save({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, ck)
         inf.DEVICE = DEV
         masks, crops = inf.run_unet(pil, ck, compute_dtype="fp32")
+    if pillow == "pillow_10_2":
+        assert calls == [(400, 600, 3)]   # the packed photo went through the graph, not the RGBX export
     for k in inf.FIELDS:
         ref = np.unpackbits(z["maskbits_" + k], axis=-1, bitorder="little").astype(bool)
         iou = orc.mask_iou(masks[k], ref)
@@ -1247,10 +1262,56 @@ def test_run_unet_masks_survive_later_calls():
             for k in inf.FIELDS:
                 assert np.array_equal(again[k], snap[k]), (j, k)
         st = inf._staging[str(inf.DEVICE)]
-        assert len(st.mask_blocks) == inf._Staging.MASK_POOL
+        assert len(st.masks.blocks) == inf._Staging.MASK_POOL
+        # one photo graph per geometry, its masks copy retargeted to each block lent
+        assert len(st.graphs) == 1 and st.retarget
         del kept, masks, again
-        blk = st.mask_block()
-        assert blk is not None   # every returned mask dropped: a block is free again
+        import gc
+        gc.collect()
+        assert all(st.masks.idle)   # every returned mask dropped: every block is free again
+
+
+def test_photo_graph_eviction_beside_batch_calls_on_another_thread():
+    """evicting photo graphs (unet_graph_destroy drains the handle) while run_unet_batch runs on
+    another thread and another stream: the destroy takes the handle's lock, so it never clears the
+    stream-order state under a forward in flight.  Every batch result equals the single-threaded one, and
+    every run_unet result too, while the LRU (shrunk to 1 geometry) evicts a graph on every call."""
+    import threading
+    from unet_mi355x import inference as inf
+    photos = _photos(4)
+    sizes = [(600, 400), (640, 480), (500, 700), (800, 600)]
+    singles = [p.resize(sz) for p, sz in zip(photos, sizes)]
+    with tempfile.TemporaryDirectory() as td:
+        ck = _save_ckpt(td)
+        inf.DEVICE = DEV
+        want_batch = inf.run_unet_batch(photos, ck, compute_dtype="mixed")
+        want_single = [inf.run_unet(p, ck, compute_dtype="mixed") for p in singles]
+        st = inf._staging[str(inf.DEVICE)]
+        old_max = st.MAX_GRAPHS
+        st.MAX_GRAPHS = 1
+        errors, stop = [], threading.Event()
+
+        def batch_worker():
+            side = torch.cuda.Stream(device=DEV)
+            try:
+                with torch.cuda.stream(side):
+                    while not stop.is_set():
+                        for a, b in zip(inf.run_unet_batch(photos, ck, compute_dtype="mixed"), want_batch):
+                            _same_result(a, b, inf.FIELDS)
+            except Exception as e:   # noqa: BLE001 - reported below
+                errors.append(repr(e))
+        th = threading.Thread(target=batch_worker)
+        th.start()
+        try:
+            for r in range(12):
+                i = r % len(singles)
+                _same_result(inf.run_unet(singles[i], ck, compute_dtype="mixed"), want_single[i], inf.FIELDS)
+                assert len(st.graphs) == 1
+        finally:
+            stop.set()
+            th.join(120)
+            st.MAX_GRAPHS = old_max
+        assert not th.is_alive() and errors == []
 
 
 def test_run_unet_batch_loose_chunks_equal_one_large_forward():

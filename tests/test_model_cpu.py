@@ -188,8 +188,9 @@ def test_copy_rgbx_equals_the_photo_pixels():
 
 def test_staging_outputs_are_one_block_in_copy_order():
     """run_unet's output buffers are carved from one block, masks | boxes | rects | sums, so the photo
-    graph copies the three small ones back as one (unet_photo_graph_create merges adjacent copies):
-    each view contiguous, of the right dtype and shape, int64 sums 8-byte aligned, no gaps."""
+    graph copies the three small ones back as one (unet_photo_graph_create merges adjacent copies; the
+    masks copy is its own node, retargeted per call): each view contiguous, of the right dtype and shape,
+    int64 sums 8-byte aligned, no gaps."""
     from unet_mi355x import inference as inf
     block = torch.empty(inf._Staging._out_bytes(), dtype=torch.uint8)
     m, b, r, s = inf._Staging._outputs(block)
@@ -207,26 +208,101 @@ def test_staging_outputs_are_one_block_in_copy_order():
     assert (s.data_ptr() - base) % 8 == 0
 
 
-def test_mask_blocks_are_reused_only_when_unreferenced(monkeypatch):
-    """run_unet's pinned mask blocks (inference._Staging.mask_block): a block is handed out again only
-    once no mask returned in it is referenced (the masks are views of it), a fifth concurrent holder
-    gets -1 (the copying path).  CPU stand-in: pinned allocation replaced by a plain one."""
+def _plain_pool(monkeypatch, size=4):
     from unet_mi355x import inference as inf
     real_empty = torch.empty
     monkeypatch.setattr(torch, "empty", lambda *a, **k: real_empty(*a, **{x: v for x, v in k.items() if x != "pin_memory"}))
-    st = inf._Staging.__new__(inf._Staging)
-    st.m = real_empty((1, 3, 8, 8), dtype=torch.uint8)
-    st.mask_blocks = []
-    i0 = st.mask_block()
-    assert i0 == 0 and st.mask_block() == 0           # idle: the same block again
-    held = {k: st.mask_blocks[0][1][j] for j, k in enumerate(inf.FIELDS)}
-    assert st.mask_block() == 1                       # block 0 is held by the masks' views
+    return inf._MaskPool((3, 8, 8), size)
+
+
+def test_mask_blocks_are_lent_until_the_last_view_dies(monkeypatch):
+    """run_unet's pinned mask blocks (inference._MaskPool): a block is lent again only once no mask returned
+    in it is alive (a weakref.finalize on the owner every view keeps alive hands it back); with every
+    block lent, take() gives None (the copying path).  CPU stand-in: pinned allocation replaced by a plain
+    one."""
+    import gc
+    from unet_mi355x import inference as inf
+    pool = _plain_pool(monkeypatch)
+    t0, a0 = pool.take()
+    assert pool.blocks[0] is t0 and a0.dtype == np.bool_ and a0.shape == (3, 8, 8)
+    held = {k: a0[j] for j, k in enumerate(inf.FIELDS)}
+    del a0
+    t1, a1 = pool.take()
+    assert t1 is pool.blocks[1]                         # block 0 is held by the masks' views
+    del a1
+    assert pool.take()[0] is pool.blocks[1]             # block 1's views are gone: lent again (and dropped)
     one = held["date"]
     del held
-    assert st.mask_block() == 1                       # one field kept: block 0 still held
+    assert pool.take()[0] is pool.blocks[1]             # one field kept: block 0 still held
     del one
-    assert st.mask_block() == 0                       # all dropped: block 0 free again
-    keep = [st.mask_blocks[st.mask_block()][1][0] for _ in range(inf._Staging.MASK_POOL)]
-    assert st.mask_block() == -1                      # every block held: the copying graph
+    gc.collect()
+    assert pool.take()[0] is pool.blocks[0]             # all dropped: block 0 free again
+    keep = [pool.take()[1][0] for _ in range(pool.size)]
+    assert len(pool.blocks) == pool.size and pool.take() is None   # every block held: the copying path
     del keep
-    assert st.mask_block() == 0
+    assert pool.take() is not None
+    # views survive a copy of the dict they came in and a numpy view of a view
+    t, a = pool.take()
+    v = a[2][1:, ::2]
+    del a
+    i = [b is t for b in pool.blocks].index(True)
+    assert not pool.idle[i]
+    del v
+    assert pool.idle[i]
+
+
+def test_mask_block_of_a_failed_call_goes_back(monkeypatch):
+    """A call that fails after taking a block (its bool array never reaches a caller) returns the block."""
+    pool = _plain_pool(monkeypatch, size=1)
+
+    def failing_call():
+        lent = pool.take()
+        raise RuntimeError("launch failed")
+    for _ in range(3):
+        try:
+            failing_call()
+        except RuntimeError:
+            pass
+        assert pool.idle == [True]
+
+
+def test_weight_tracking_is_scoped_to_the_unet_tree():
+    """the re-pack signature's tensor list is invalidated by the UNet tree's own modules (tracked
+    subclasses of the reference's layer classes), not by process-global torch hooks: importing the package
+    installs none, a foreign module's registrations leave the epoch alone, and every way of replacing a
+    tensor of the tree -- parameter / buffer assignment, a replaced sub-module, _apply on a leaf --
+    changes the UNet's signature."""
+    import torch.nn as nn
+    import torch.nn.modules.module as mm
+    from unet_mi355x import model as mdl
+    for d in ("_global_parameter_registration_hooks", "_global_buffer_registration_hooks",
+              "_global_module_registration_hooks"):
+        assert not getattr(mm, d, {}), d
+    m = mdl.UNet(3, 3)
+    assert type(m.down1.net[0]).__name__ == "Conv2d" and isinstance(m.down1.net[0], nn.Conv2d)
+    assert "Conv2d(3, 64, kernel_size=(3, 3)" in repr(m)
+    assert len(m.state_dict()) == 136
+    sig0 = m._signature()
+    e0 = mdl._TREE_EPOCH[0]
+    foreign = nn.Linear(3, 3)
+    foreign.weight = nn.Parameter(torch.zeros(3, 3))
+    foreign.register_buffer("b", torch.zeros(1))
+    assert mdl._TREE_EPOCH[0] == e0                     # other modules of the process are not touched
+    assert m._signature() == sig0
+    m.down2.net[0].weight = nn.Parameter(torch.zeros_like(m.down2.net[0].weight))
+    sig1 = m._signature()
+    assert sig1 != sig0
+    m.conv3.net[4].running_mean = torch.zeros(256)      # buffer assignment (no register_buffer call)
+    sig2 = m._signature()
+    assert sig2 != sig1
+    m.out_conv.float()                                   # _apply on a leaf (no change of storage here)
+    m.up2 = mdl.ConvTranspose2d(256, 128, 2, stride=2)   # a replaced sub-module
+    sig3 = m._signature()
+    assert sig3 != sig2
+    with torch.no_grad():
+        m.up2.bias.add_(1)                               # in-place update: _version
+    assert m._signature() != sig3
+    m.up1 = nn.ConvTranspose2d(128, 64, 2, stride=2)     # a plain module: the signature walks the live tree
+    s4 = m._signature()
+    m.up1.weight = nn.Parameter(torch.zeros_like(m.up1.weight))
+    assert not m._sig_tracked and m._signature() != s4

@@ -154,6 +154,11 @@ struct unet_graph {
   ResampleStore rs;
   uint8_t* pp_tmp = nullptr;
   int* crop_sync = nullptr;   // the crop sums' sync entries (n_classes, zeroed at capture)
+  // the photo graph's masks copy node (unet_photo_graph_set_masks retargets its host destination)
+  hipGraphNode_t masks_node = nullptr;
+  void* masks_dst = nullptr;
+  const void* masks_src = nullptr;
+  size_t masks_bytes = 0;
 };
 
 namespace {
@@ -1479,16 +1484,21 @@ int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih
     hipError_t e = hipMalloc((void**)&gr->pp_tmp, tmp);
     if (e != hipSuccess) rc = fail(UNET_ENOMEM, std::string("preprocess buffer: ") + hipGetErrorString(e));
   }
-  if (!rc) {   // the crop sums' sync entries, idle (zero)
-    const size_t bytes = (size_t)h->cfg.n_classes * kSyncInts * sizeof(int);
-    hipError_t e = hipMalloc((void**)&gr->crop_sync, bytes);
-    if (e == hipSuccess) e = hipMemset(gr->crop_sync, 0, bytes);
+  const size_t sync_bytes = (size_t)h->cfg.n_classes * kSyncInts * sizeof(int);
+  if (!rc) {   // the crop sums' sync entries
+    hipError_t e = hipMalloc((void**)&gr->crop_sync, sync_bytes);
     if (e != hipSuccess) rc = fail(UNET_ENOMEM, std::string("crop sync entries: ") + hipGetErrorString(e));
   }
   hipStream_t cs = nullptr;
   if (!rc) {
     hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
     if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  if (!rc) {   // idle (zero) before the capture: set on the capture stream and waited for, so no replay on any
+               // caller stream can start before it (a null-stream memset is asynchronous to the host)
+    hipError_t e = hipMemsetAsync(gr->crop_sync, 0, sync_bytes, cs);
+    if (e == hipSuccess) e = hipStreamSynchronize(cs);
+    if (e != hipSuccess) rc = fail(UNET_EHIP, std::string("crop sync entries: ") + hipGetErrorString(e));
   }
   if (!rc) {
     hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
@@ -1527,7 +1537,20 @@ int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih
           else
             copies.push_back({d, sp, bytes});
         };
-        add(h_masks, masks, mbytes);
+        // the masks copy stays a node of its own (never merged): unet_photo_graph_set_masks retargets it
+        if (h_masks && e == hipSuccess) {
+          e = hipMemcpyAsync(h_masks, masks, mbytes, hipMemcpyDeviceToHost, cs);
+          hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+          const hipGraphNode_t* deps = nullptr;
+          size_t ndeps = 0;
+          if (e == hipSuccess) e = hipStreamGetCaptureInfo_v2(cs, &st, nullptr, nullptr, &deps, &ndeps);
+          if (e == hipSuccess && ndeps == 1) {   // the node just captured
+            gr->masks_node = deps[0];
+            gr->masks_dst = h_masks;
+            gr->masks_src = masks;
+            gr->masks_bytes = mbytes;
+          }
+        }
         add(h_boxes, boxes, (size_t)ncls * 16);
         add(h_rects, rects, (size_t)ncls * 16);
         add(h_sums, sums, (size_t)ncls * 8);
@@ -1551,6 +1574,19 @@ int unet_photo_graph_create(unet_handle* h, const void* h_img, void* img, int ih
   }
   gr->generation = h->generation;
   *out = gr;
+  return UNET_OK;
+}
+
+int unet_photo_graph_set_masks(unet_graph* gr, void* h_masks) {
+  if (!gr || !gr->exec || !h_masks) return fail(UNET_EINVAL, "null argument");
+  if (!gr->masks_node) return fail(UNET_ESTATE, "graph has no retargetable masks copy (not a photo graph with h_masks)");
+  if (h_masks == gr->masks_dst) return UNET_OK;
+  DeviceGuard g(gr->h->cfg.device);
+  // the next replay copies into h_masks; launches already enqueued keep their destination
+  hipError_t e = hipGraphExecMemcpyNodeSetParams1D(gr->exec, gr->masks_node, h_masks, gr->masks_src, gr->masks_bytes,
+                                                   hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return fail(UNET_EHIP, std::string("hipGraphExecMemcpyNodeSetParams1D: ") + hipGetErrorString(e));
+  gr->masks_dst = h_masks;
   return UNET_OK;
 }
 
@@ -1685,6 +1721,9 @@ int unet_block_create(const unet_block_config* cfg, unet_block** out) {
   if (cout <= 0 || cout % 64 || (first && cout != 64) || (!first && (cin <= 0 || cin % 32)))
     return fail(UNET_ESHAPE, "DoubleConv(in_ch, out_ch) runs natively for in_ch in {1, 3} with out_ch = 64, or in_ch "
                              "a multiple of 32 and out_ch a multiple of 64 (every block of the reference UNet)");
+  if (cfg->dtype != UNET_DTYPE_F32 && cout != 64 && cout % 128)   // the 16-bit rings tile 64 or 128-row groups
+    return fail(UNET_ESHAPE, "DoubleConv(in_ch, out_ch) on the 16-bit plans needs out_ch = 64 or a multiple of 128 "
+                             "(the 128-row MFMA ring tiles); fp32 takes any multiple of 64");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (cfg->device < 0 || cfg->device >= ndev) return fail(UNET_EINVAL, "bad device ordinal");

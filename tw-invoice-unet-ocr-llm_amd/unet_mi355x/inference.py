@@ -20,8 +20,8 @@ from __future__ import annotations
 
 import ctypes
 import os
-import sys
 import threading
+import weakref
 from collections import OrderedDict
 
 import numpy as np
@@ -199,20 +199,53 @@ def copy_rgbx(pil_img: Image.Image, dst_ptr: int, capacity: int):
     return (h, w, 4)
 
 
-def _refs(blk):
-    """Reference counts of a mask block's bool array and of the uint8 array its views have as base."""
-    return sys.getrefcount(blk[1]), sys.getrefcount(blk[2])
+class _MaskPool:
+    """Pinned [n_fields, 512, 512] blocks that run_unet returns its masks in (the photo graph DMAs the masks
+    straight into one, and run_unet hands out bool views of it instead of copying 768 KB out of a shared
+    pinned buffer: about 27 us per call on the GPU box's host, the data being cold after the DMA).
+
+    A block is lent with an owner object (a ctypes array over the pinned memory) that the returned bool
+    array is built on: every mask view keeps it alive, and a weakref.finalize on it hands the block back
+    when the last view dies -- however the caller drops them, and also when run_unet fails after taking
+    the block.  At most ``size`` blocks; when all are lent, ``take`` returns None (run_unet then copies)."""
+
+    def __init__(self, shape, size: int = 4):
+        self.shape, self.size = tuple(shape), size
+        self.blocks: list = []    # pinned uint8 tensors
+        self.idle: list = []      # per block: not lent
+
+    def take(self):
+        """(pinned block tensor, bool array over it whose views hand it back when they are all gone), or None."""
+        for i, ok in enumerate(self.idle):
+            if ok:
+                break
+        else:
+            if len(self.blocks) >= self.size:
+                return None
+            self.blocks.append(torch.empty(self.shape, dtype=torch.uint8, pin_memory=True))
+            self.idle.append(True)
+            i = len(self.blocks) - 1
+        self.idle[i] = False
+        t = self.blocks[i]
+        owner = (ctypes.c_ubyte * t.numel()).from_address(t.data_ptr())
+        arr = np.frombuffer(owner, dtype=np.bool_).reshape(self.shape)
+        weakref.finalize(owner, self._give_back, i)
+        return t, arr
+
+    def _give_back(self, i: int):
+        self.idle[i] = True   # one list item store: safe from the finaliser's thread
 
 
 class _Staging:
     """Buffers of one device's run_unet calls, reused across calls: the photo (pinned host + device),
     the network input, the u8 masks and boxes, the crop statistics (device + pinned host), so a call
     allocates nothing and makes ONE stream synchronisation; the pinned mask blocks run_unet returns its
-    masks in (mask_block); and the photo graphs captured over them (one per photo geometry and mask
-    block, of one model, LRU-bounded), which stay valid while these buffers do."""
+    masks in (_MaskPool); and the photo graphs captured over them -- one per photo geometry of one model,
+    LRU-bounded, its masks copy retargeted per call to the block lent (unet_photo_graph_set_masks) --,
+    which stay valid while these buffers do."""
 
-    MASK_POOL = 4   # pinned mask blocks handed out as run_unet's masks (no host copy), see mask_block
-    MAX_GRAPHS = 2 * (MASK_POOL + 1)   # a geometry's graphs: one per mask block + the copying one
+    MASK_POOL = 4     # pinned mask blocks lent as run_unet's masks (no host copy), see _MaskPool
+    MAX_GRAPHS = 8    # photo geometries with a captured graph (LRU)
 
     def __init__(self, device):
         self.device = torch.device(device)
@@ -220,12 +253,13 @@ class _Staging:
         self.h_img = self.d_img = None
         self.x = torch.empty((1, 3, IMG_SIZE, IMG_SIZE), dtype=torch.float32, device=self.device)
         # the outputs, u8 masks | boxes | crop rectangles | crop pixel sums, carved from one device and
-        # one pinned host block in the same order: the photo graph copies them back as one
+        # one pinned host block in the same order: the photo graph copies boxes | rects | sums back as one
         self.m, self.b, self.r, self.s = self._outputs(torch.empty(self._out_bytes(), dtype=torch.uint8,
                                                                    device=self.device))
         self.hm, self.hb, self.hr, self.hs = self._outputs(torch.empty(self._out_bytes(), dtype=torch.uint8, pin_memory=True))
-        self.graphs: OrderedDict = OrderedDict()   # ((ih, iw, c), block) -> (model, native.Graph)
-        self.mask_blocks: list = []                # pinned [n, 512, 512] bool arrays, see mask_block
+        self.graphs: OrderedDict = OrderedDict()   # key -> (model, native.Graph); key = (ih, iw, c)
+        self.masks = _MaskPool(self.m.shape[1:], self.MASK_POOL)
+        self.retarget = True   # False: this HIP runtime refused to retarget a masks copy; one graph per target
 
     @staticmethod
     def _out_bytes():
@@ -276,40 +310,36 @@ class _Staging:
         dst.view(-1).copy_(self.h_img[:arr.size], non_blocking=True)
         return dst
 
-    def mask_block(self):
-        """Index of a pinned [n_fields, 512, 512] bool block no caller holds any more (the masks run_unet
-        returned in it are views of it, so while one is alive its reference counts stay up), or -1 when
-        all MASK_POOL blocks are held.  The photo graph of that block DMAs the masks straight into it and
-        run_unet returns views instead of copying 768 KB out of the shared pinned buffer (≈27 µs per call
-        on the GPU box's host: the data is cold after the DMA); -1: the graph copying into the shared
-        buffer, and run_unet copies."""
-        for i, blk in enumerate(self.mask_blocks):
-            if _refs(blk) == blk[3]:
-                return i
-        if len(self.mask_blocks) < self.MASK_POOL:
-            t = torch.empty(self.m.shape[1:], dtype=torch.uint8, pin_memory=True)
-            u = t.numpy()
-            blk = [t, u.view(np.bool_), u, None]
-            del u
-            blk[3] = _refs(blk)   # idle: referenced only from here (numpy views of the bool array name u as base)
-            self.mask_blocks.append(tuple(blk))
-            return len(self.mask_blocks) - 1
-        return -1
-
     def drop_graphs(self):
         for _, g in self.graphs.values():
             g.close()
         self.graphs.clear()
 
-    def photo_graph(self, model, img: torch.Tensor, blk: int = -1):
-        """The photo graph of (model, photo geometry, mask block): upload + resize + forward (masks, boxes) +
-        crop statistics + copies back (unet_photo_graph_create) -- the masks into mask block blk, or
-        into the shared pinned buffer (blk = -1) --, captured at the first call of the combination."""
-        key = (tuple(img.shape), blk)
+    def drop_graph(self, key):
+        e = self.graphs.pop(key, None)
+        if e is not None:
+            e[1].close()
+
+    def graph_key(self, img: torch.Tensor, target: torch.Tensor):
+        return tuple(img.shape) if self.retarget else (tuple(img.shape), target.data_ptr())
+
+    def photo_graph(self, model, img: torch.Tensor, target: torch.Tensor):
+        """The photo graph of (model, photo geometry): upload + resize + forward (masks, boxes) + crop
+        statistics + copies back (unet_photo_graph_create), captured at the first call of the geometry, its
+        masks copy pointed at ``target`` (a lent mask block, or the shared pinned buffer)."""
+        key = self.graph_key(img, target)
         e = self.graphs.get(key)
         if e is not None and e[0] is model:
             self.graphs.move_to_end(key)
-            return e[1]
+            g = e[1]
+            if self.retarget and g.masks_ptr != target.data_ptr():
+                try:
+                    g.set_masks(target.view(self.hm.shape))
+                except RuntimeError:   # this runtime cannot retarget a captured copy: one graph per target
+                    self.retarget = False
+                    self.drop_graphs()
+                    return self.photo_graph(model, img, target)
+            return g
         if any(m is not model for m, _ in self.graphs.values()):
             # another model (a re-loaded checkpoint or another precision plan): the model cache holds one
             # model, so drop its graphs -- they keep its handle (workspace, weights) alive
@@ -317,11 +347,10 @@ class _Staging:
         h = model.native_handle(self.device)
         h.reserve(1, IMG_SIZE, IMG_SIZE)
         img3 = img if img.dim() == 3 else img.unsqueeze(-1)
-        hm = self.mask_blocks[blk][0].view(self.hm.shape) if blk >= 0 else self.hm
         g = h.photo_graph(self.h_img, img3, self.x, self.m, native.MASK_U8, self.b, CROP_PAD, self.r, self.s,
-                          hm, self.hb, self.hr, self.hs)
+                          target.view(self.hm.shape), self.hb, self.hr, self.hs)
         self.graphs[key] = (model, g)
-        while len(self.graphs) > self.MAX_GRAPHS:
+        while len(self.graphs) > self.MAX_GRAPHS * (1 if self.retarget else self.MASK_POOL + 1):
             self.graphs.popitem(last=False)[1][1].close()
         return g
 
@@ -345,17 +374,18 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
             # fused sigmoid + threshold + per-field boxes, and the crop statistics, all on the device as
             # one graph per photo geometry: one launch, one synchronisation
             img, ch = st.stage_photo(pil_img)
-            blk = st.mask_block()
-            g = st.photo_graph(model, img, blk)
+            lent = st.masks.take()   # (pinned block, bool array over it) or None: all blocks are held
+            target = lent[0] if lent is not None else st.hm[0]
+            g = st.photo_graph(model, img, target)
             try:
                 g.launch(stream.cuda_stream)
             except RuntimeError:   # stale (the cached model's workspace grew, e.g. run_unet_batch): capture again
-                st.graphs.pop((tuple(img.shape), blk), None)
-                g.close()
-                st.photo_graph(model, img, blk).launch(stream.cuda_stream)
+                st.drop_graph(st.graph_key(img, target))
+                st.photo_graph(model, img, target).launch(stream.cuda_stream)
             stream.synchronize()
-            # the kernel writes 0 / 1 bytes: bool views of the block, or a copy out of the shared buffer
-            m = st.mask_blocks[blk][1] if blk >= 0 else st.hm.numpy()[0].view(np.bool_).copy()
+            # the kernel writes 0 / 1 bytes: bool views of the lent block, or a copy out of the shared buffer
+            m = lent[1] if lent is not None else st.hm.numpy()[0].view(np.bool_).copy()
+            del lent
             rects, sums = st.hr.numpy().copy(), st.hs.numpy().copy()
             masks = {k: m[i] for i, k in enumerate(FIELDS)}
             return masks, {k: crop_from_stats(pil_img, rects[i], sums[i], ch) for i, k in enumerate(FIELDS)}

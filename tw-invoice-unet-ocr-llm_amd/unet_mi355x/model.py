@@ -16,29 +16,84 @@ import threading
 
 import torch
 import torch.nn as nn
-import torch.nn.modules.module as _mm
 
 from . import native
 
 DEFAULT_DTYPE = os.environ.get("UNET_MI355X_DTYPE", "fp32")
 
-# Bumped whenever any module anywhere registers a parameter, buffer or sub-module, or a UNet /
-# DoubleConv converts its tensors (_apply: .to / .cuda / .half): the cached list of tensors whose
-# (data_ptr, _version) signature decides re-packing is then rebuilt.  Between such events the
-# per-forward check reads 136 cached tensors instead of rebuilding state_dict().
+# Bumped whenever a module of a UNet's tree (the _Tracked classes below) changes its parameters, buffers or
+# children -- attribute assignment, register_parameter / register_buffer / add_module, deletion -- or converts
+# its tensors (_apply: .to / .cuda / .half): the cached list of tensors whose (data_ptr, _version) signature
+# decides re-packing is then rebuilt.  Between such events the per-forward check reads 136 cached tensors
+# instead of rebuilding state_dict().  Scoped to these classes: no process-global torch hooks, so other
+# modules of the app process (EasyOCR's) are never touched.
 _TREE_EPOCH = [0]
 
 
 def _bump_epoch(*_args):
-    _TREE_EPOCH[0] += 1   # returns None: the hooks never replace what is registered
+    _TREE_EPOCH[0] += 1
 
 
-_mm.register_module_parameter_registration_hook(_bump_epoch)
-_mm.register_module_buffer_registration_hook(_bump_epoch)
-_mm.register_module_module_registration_hook(_bump_epoch)
+class _Tracked:
+    """Mixin of every module class in the UNet tree: any change to this module's own tensors or children
+    bumps _TREE_EPOCH.  A tree holding a module without it (a user-assigned plain nn.Module) makes
+    UNet._signature walk the live tree on every call instead of trusting the cached list."""
+
+    def __setattr__(self, name, value):
+        super().__setattr__(name, value)
+        _bump_epoch()
+
+    def __delattr__(self, name):
+        super().__delattr__(name)
+        _bump_epoch()
+
+    def register_parameter(self, name, param):
+        super().register_parameter(name, param)
+        _bump_epoch()
+
+    def register_buffer(self, name, tensor, persistent=True):
+        super().register_buffer(name, tensor, persistent)
+        _bump_epoch()
+
+    def add_module(self, name, module):
+        super().add_module(name, module)
+        _bump_epoch()
+
+    def register_module(self, name, module):
+        self.add_module(name, module)
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        _bump_epoch()
+        return out
 
 
-class DoubleConv(nn.Module):
+# the reference's layer classes (same constructor, parameters, state_dict keys and repr), tracked
+class Conv2d(_Tracked, nn.Conv2d):
+    pass
+
+
+class BatchNorm2d(_Tracked, nn.BatchNorm2d):
+    pass
+
+
+class ReLU(_Tracked, nn.ReLU):
+    pass
+
+
+class Sequential(_Tracked, nn.Sequential):
+    pass
+
+
+class MaxPool2d(_Tracked, nn.MaxPool2d):
+    pass
+
+
+class ConvTranspose2d(_Tracked, nn.ConvTranspose2d):
+    pass
+
+
+class DoubleConv(_Tracked, nn.Module):
     """unet_model.py:6-20: (conv3x3, BN, ReLU) x 2 -- the same parameters (and state_dict keys).
 
     Inside UNet.forward the blocks run fused with pooling / concat / head (the whole-network native
@@ -49,13 +104,13 @@ class DoubleConv(nn.Module):
 
     def __init__(self, in_ch: int, out_ch: int, compute_dtype: str | None = None):
         super().__init__()
-        self.net = nn.Sequential(
-            nn.Conv2d(in_ch, out_ch, kernel_size=3, padding=1),
-            nn.BatchNorm2d(out_ch),
-            nn.ReLU(inplace=True),
-            nn.Conv2d(out_ch, out_ch, kernel_size=3, padding=1),
-            nn.BatchNorm2d(out_ch),
-            nn.ReLU(inplace=True),
+        self.net = Sequential(
+            Conv2d(in_ch, out_ch, kernel_size=3, padding=1),
+            BatchNorm2d(out_ch),
+            ReLU(inplace=True),
+            Conv2d(out_ch, out_ch, kernel_size=3, padding=1),
+            BatchNorm2d(out_ch),
+            ReLU(inplace=True),
         )
         self.in_ch, self.out_ch = in_ch, out_ch
         self.compute_dtype = compute_dtype
@@ -95,11 +150,6 @@ class DoubleConv(nn.Module):
             blk.forward(x, y, torch.cuda.current_stream(x.device).cuda_stream)
         return y
 
-    def _apply(self, fn, *args, **kwargs):
-        out = super()._apply(fn, *args, **kwargs)
-        _bump_epoch()
-        return out
-
     def close(self):
         for b in self._blocks.values():
             b.close()
@@ -107,7 +157,7 @@ class DoubleConv(nn.Module):
         self._packed_sig.clear()
 
 
-class UNet(nn.Module):
+class UNet(_Tracked, nn.Module):
     """unet_model.UNet(n_channels=3, n_classes=3) with an MI355X forward.
 
     compute_dtype: "fp32" (default; exact fp32 MFMA, reference semantics), "bf16" or
@@ -135,17 +185,17 @@ class UNet(nn.Module):
         self.down2 = DoubleConv(64, 128, cd)
         self.down3 = DoubleConv(128, 256, cd)
         self.down4 = DoubleConv(256, 512, cd)
-        self.pool = nn.MaxPool2d(2)
+        self.pool = MaxPool2d(2)
         self.bottleneck = DoubleConv(512, 1024, cd)
-        self.up4 = nn.ConvTranspose2d(1024, 512, 2, stride=2)
+        self.up4 = ConvTranspose2d(1024, 512, 2, stride=2)
         self.conv4 = DoubleConv(1024, 512, cd)
-        self.up3 = nn.ConvTranspose2d(512, 256, 2, stride=2)
+        self.up3 = ConvTranspose2d(512, 256, 2, stride=2)
         self.conv3 = DoubleConv(512, 256, cd)
-        self.up2 = nn.ConvTranspose2d(256, 128, 2, stride=2)
+        self.up2 = ConvTranspose2d(256, 128, 2, stride=2)
         self.conv2 = DoubleConv(256, 128, cd)
-        self.up1 = nn.ConvTranspose2d(128, 64, 2, stride=2)
+        self.up1 = ConvTranspose2d(128, 64, 2, stride=2)
         self.conv1 = DoubleConv(128, 64, cd)
-        self.out_conv = nn.Conv2d(64, n_classes, kernel_size=1)
+        self.out_conv = Conv2d(64, n_classes, kernel_size=1)
         nn.init.constant_(self.out_conv.bias, -4)  # unet_model.py:52-53
 
         self._handles: dict[int, native.Handle] = {}
@@ -153,17 +203,13 @@ class UNet(nn.Module):
         self._lock = threading.Lock()
         self._sig_tensors = None
         self._sig_epoch = -1
+        self._sig_tracked = False
         # set by the drop-in's private model cache (inference._cached_model), whose model nobody can
         # reach to modify: once packed, its handle skips the per-call weight signature (136 tensors,
         # ~40-50 us of host time on the batch-1 call path)
         self._frozen = False
 
     # ------------------------------------------------------------------ native plumbing
-    def _apply(self, fn, *args, **kwargs):
-        out = super()._apply(fn, *args, **kwargs)
-        _bump_epoch()
-        return out
-
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         """nn.Module.load_state_dict; every packed handle re-packs at its next use (also when frozen)."""
         out = super().load_state_dict(state_dict, strict=strict, assign=assign)
@@ -176,7 +222,8 @@ class UNet(nn.Module):
         """(data_ptr, _version) of every state_dict tensor: changes on any in-place update
         (load_state_dict, optimizer steps, ``with no_grad(): p.add_``), on .to() / .data
         replacement and on re-registration (the cached tensor list is rebuilt then)."""
-        if self._sig_epoch != _TREE_EPOCH[0] or self._sig_tensors is None:
+        if self._sig_epoch != _TREE_EPOCH[0] or self._sig_tensors is None or not self._sig_tracked:
+            self._sig_tracked = all(isinstance(m, _Tracked) for m in self.modules())
             self._sig_tensors = list(self.state_dict(keep_vars=True).values())
             self._sig_epoch = _TREE_EPOCH[0]
         return tuple((t.data_ptr(), t._version) for t in self._sig_tensors)
@@ -192,7 +239,8 @@ class UNet(nn.Module):
             # frozen (the drop-in's private cache): skip the 136-tensor signature while nothing was
             # re-registered or converted anywhere (_TREE_EPOCH) and no load_state_dict ran (it clears
             # _packed_sig); otherwise check it as usual
-            if h is not None and self._frozen and idx in self._packed_sig and self._sig_epoch == _TREE_EPOCH[0]:
+            if (h is not None and self._frozen and idx in self._packed_sig and self._sig_epoch == _TREE_EPOCH[0]
+                    and self._sig_tracked):
                 return h
             if h is None:
                 h = native.Handle(self.n_channels, self.n_classes, self.compute_dtype, idx,

@@ -24,7 +24,7 @@ DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16
 MASK_NONE, MASK_U8, MASK_BITS = 0, 1, 2
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
 COMM_ID_BYTES = 128
-ABI_VERSION = 4   # include/unet_mi355x.h UNET_ABI_VERSION
+ABI_VERSION = 5   # include/unet_mi355x.h UNET_ABI_VERSION
 IN_F32, IN_U8 = 0, 1
 
 # every function include/unet_mi355x.h declares: name -> (restype, argtypes)
@@ -83,6 +83,7 @@ SIGNATURES = {
     "unet_small_batch_limit": (_i, [_vp]),
     "unet_photo_graph_create": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _i, _vp, _i, _vp, ctypes.c_double, _vp, _vp,
                                      _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+    "unet_photo_graph_set_masks": (_i, [_vp, _vp]),
     "unet_forward_timed": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
     "unet_debug_fetch": (_i, [_vp, ctypes.c_char_p, _vp, ctypes.POINTER(_sz), _vp]),
     "unet_graph_create": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _i, ctypes.POINTER(_vp)]),
@@ -186,7 +187,9 @@ class Handle:
         h = ctypes.c_void_p()
         check(self.lib.unet_create(ctypes.byref(cfg), ctypes.byref(h)), "unet_create")
         self._h = h
-        self.lock = threading.Lock()
+        # re-entrant: a Graph's close (unet_graph_destroy drains the handle's pending work and clears its
+        # stream-order state) takes it too, and may run from a garbage collection inside a locked call
+        self.lock = threading.RLock()
         self._graphs = weakref.WeakSet()   # captured graphs die before the handle
 
     def load_weights(self, state_dict) -> None:
@@ -299,7 +302,8 @@ class Handle:
                                                    rects.data_ptr(), sums.data_ptr(), ptr(h_masks), ptr(h_boxes),
                                                    ptr(h_rects), ptr(h_sums), ctypes.byref(g)),
                   "unet_photo_graph_create")
-        gr = Graph(self, g, (h_img, img, x, masks, boxes, rects, sums, h_masks, h_boxes, h_rects, h_sums))
+        gr = Graph(self, g, (h_img, img, x, masks, boxes, rects, sums, h_masks, h_boxes, h_rects, h_sums),
+                   masks_ptr=0 if h_masks is None else h_masks.data_ptr())
         self._graphs.add(gr)
         return gr
 
@@ -362,8 +366,10 @@ class Handle:
         for gr in list(getattr(self, "_graphs", ())):
             gr.close()
         if getattr(self, "_h", None):
-            self.lib.unet_destroy(self._h)
-            self._h = None
+            with self.lock:
+                if self._h:
+                    self.lib.unet_destroy(self._h)
+                    self._h = None
 
     def __del__(self):
         try:
@@ -415,17 +421,35 @@ class Block:
 class Graph:
     """A captured forward (unet_graph_*); keeps its buffers alive; replay with ``launch``."""
 
-    def __init__(self, handle: Handle, g: ctypes.c_void_p, buffers):
+    def __init__(self, handle: Handle, g: ctypes.c_void_p, buffers, masks_ptr: int = 0):
         self.handle, self._g, self._buffers = handle, g, buffers
+        self.masks_ptr = masks_ptr   # a photo graph's current masks copy destination (host pointer)
 
     def launch(self, stream: int) -> None:
         with self.handle.lock:
             check(self.handle.lib.unet_graph_launch(self._g, stream), "unet_graph_launch")
 
+    def set_masks(self, h_masks: torch.Tensor) -> None:
+        """unet_photo_graph_set_masks: the next replays copy the masks into ``h_masks`` (pinned, contiguous,
+        the size of the masks the graph was captured with)."""
+        if h_masks.device.type != "cpu" or not h_masks.is_pinned() or not h_masks.is_contiguous():
+            raise ValueError("h_masks must be a contiguous pinned CPU tensor")
+        cur = self._buffers[7]
+        if cur is None or h_masks.numel() * h_masks.element_size() != cur.numel() * cur.element_size():
+            raise ValueError("h_masks must have the size of the graph's masks buffer")
+        with self.handle.lock:
+            check(self.handle.lib.unet_photo_graph_set_masks(self._g, h_masks.data_ptr()), "unet_photo_graph_set_masks")
+        self._masks_target = h_masks   # kept alive while the graph may copy into it
+        self.masks_ptr = h_masks.data_ptr()
+
     def close(self) -> None:
+        """unet_graph_destroy under the handle's lock: it drains the handle (reads and clears the stream-order
+        state a forward on another thread and stream sets), so it must not run beside a call of the handle."""
         if getattr(self, "_g", None):
-            self.handle.lib.unet_graph_destroy(self._g)
-            self._g = None
+            with self.handle.lock:
+                if self._g:
+                    self.handle.lib.unet_graph_destroy(self._g)
+                    self._g = None
 
     def __del__(self):
         try:
