@@ -34,7 +34,8 @@ extern "C" {
 
 #define UNET_ABI_VERSION 5   /* 2: unet_forward requires unet_reserve; Cfg renumbered; fp16 range check. 3: unet_crop_stats.
                                  4: unet_launch_label_at, unet_small_batch_limit, unet_photo_graph_create, unet_block_*
-                                 5: unet_photo_graph_set_masks (the masks copy is its own node) */
+                                 5: unet_photo_graph_set_masks (the masks copy is its own node); UNET_DTYPE_F32 as
+                                    three bf16 terms, UNET_DTYPE_F32_EXACT the exact-fp32 MFMA */
 
 /* error codes */
 #define UNET_OK 0
@@ -45,7 +46,12 @@ extern "C" {
 #define UNET_ESTATE (-5)     /* call out of order (e.g. forward before weights)       */
 #define UNET_EKEY (-6)       /* state_dict key missing / unexpected / wrong shape      */
 
-/* compute / storage dtype of the activations and packed weights (accumulation is fp32) */
+/* compute / storage dtype of the activations and packed weights (accumulation is fp32).
+ * UNET_DTYPE_F32: fp32 storage and weights; every product of the 3x3 and ConvTranspose layers computed as
+ * three bf16 terms per operand (x = hi + mid + lo, 6 bf16 MFMA products per K block, fp32 accumulation):
+ * fp32 accuracy (the reference's fp32 forward within 2e-5 of the logit scale, tests/test_forward_gpu.py)
+ * on the 2.5 PFLOP/s bf16 pipe.  UNET_DTYPE_F32_EXACT: the same plan on the exact-fp32 MFMA
+ * (v_mfma_f32_16x16x4_f32, 157 TFLOP/s). */
 #define UNET_DTYPE_F32 0
 #define UNET_DTYPE_BF16 1
 #define UNET_DTYPE_F16 2
@@ -55,6 +61,7 @@ extern "C" {
  * refuses (UNET_EINVAL) a checkpoint whose BN-folded weights or biases exceed that at an fp16
  * level; activations beyond it would become inf -- use BF16 (fp32's range) or F32 for such nets. */
 #define UNET_DTYPE_MIXED 3
+#define UNET_DTYPE_F32_EXACT 4
 
 /* input layouts / dtypes accepted by unet_forward */
 #define UNET_LAYOUT_NCHW 0   /* [N][n_channels][H][W] (the reference's torch layout)             */

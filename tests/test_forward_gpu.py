@@ -875,17 +875,14 @@ def test_preprocess_geometry_cache_is_bounded():
 @pytest.mark.parametrize("pillow", ["current", "pillow_10_2"])
 def test_run_unet_boundary_matches_reference_golden(pillow, monkeypatch):
     """inference.run_unet (drop-in) on the golden 600x400 photo vs the reference's masks/crops.
-    "pillow_10_2": the reference's pinned Pillow (requirements.txt:3) has no Arrow export and the raw
-    encoder is treated as unavailable too, so run_unet's photo graph takes the packed-photo path
-    (np.asarray, 3 bytes per pixel) -- same masks and crops."""
+    "pillow_10_2": the reference's pinned Pillow (requirements.txt:3) has no Arrow export, and the photo is
+    packed by plain np.asarray (no raw-encoder pass), so run_unet's photo graph takes the packed-photo path
+    (3 bytes per pixel) -- same masks and crops."""
     from PIL import Image
     from unet_mi355x import inference as inf
     if pillow == "pillow_10_2":
-        monkeypatch.setattr(inf, "copy_rgbx", lambda *a, **k: None)
-
-        def no_encoder(*a, **k):
-            raise AttributeError("_getencoder")
-        monkeypatch.setattr(inf.Image, "_getencoder", no_encoder)
+        monkeypatch.setattr(inf, "copy_rgbx", lambda *a, **k: None)          # no Arrow export
+        monkeypatch.setattr(inf, "photo_array", lambda im: np.asarray(im))   # the plain packing, no raw-encoder pass
         calls = []
         real_stage = inf._Staging.stage
         monkeypatch.setattr(inf._Staging, "stage", lambda self, arr: calls.append(arr.shape) or real_stage(self, arr))

@@ -80,6 +80,7 @@ struct Layer {
   DType dtq = DType::BF16;   // pooled-map type (EPI_POOL layers)
   void* w = nullptr;         // packed weights
   float* b = nullptr;        // [ctot] natural order
+  int x3 = 0;                // fp32 plan: operands as three bf16 terms (IgemmArgs::x3; 2 = pre-split packing)
 };
 
 // Device coefficient tables of one resize geometry (unet_preprocess), owned by the handle.
@@ -136,6 +137,7 @@ struct unet_handle {
   // (UNET_MI355X_KSPLIT_FORCE="i:ks,...", i = 3x3 layer 0..16 or 17 + ConvTranspose 0..3; 0 = auto;
   // ks + 100 = ks slices on 64-row tiles of the 8-wave ring)
   int ksplit_max = 32;
+  int f32x3 = 0;   // fp32 plan: 1 = operands as three bf16 terms on the bf16 MFMA pipe (IgemmArgs::x3)
   int ksplit_force[21] = {};
   void* part = nullptr;   // the current forward's partial buffer (workspace region Buffers::part)
   // mask-box sync entries (launch_mask_boxes: kSyncInts ints per (image, field), idle between
@@ -211,7 +213,7 @@ const int kUpCh[4][2] = {{1024, 512}, {512, 256}, {256, 128}, {128, 64}};
 // 0.9990.  fp16 and bf16 run the same MFMA rate on gfx950.
 DType level_dtype(int dtype, int level) {
   switch (dtype) {
-    case UNET_DTYPE_F32: return DType::F32;
+    case UNET_DTYPE_F32: case UNET_DTYPE_F32_EXACT: return DType::F32;
     case UNET_DTYPE_F16: return DType::F16;
     case UNET_DTYPE_MIXED: return level <= 1 ? DType::F16 : DType::BF16;
     default: return DType::BF16;
@@ -444,7 +446,48 @@ void pack_first_mfma(DType t0, const std::vector<double>& w, int C, std::vector<
 // Ring kernels (cfg_is_ring) take the same rows in step order instead: per row tile of BR rows,
 // step s = (c / BKE) * 9 + tap holds a contiguous [BR][BKE] block (BKE = 64 bytes of K), so
 // packed[((ct * S + s) * BR + rho % BR) * BKE + c % BKE], S = 9 * cin / BKE.
+// fp32 as three bf16 terms (round to nearest even, each difference exact in fp32): the device's split3_bf16
+void split3_host(float v, uint16_t (&t)[3]) {
+  t[0] = f32_to_bf16(v);
+  float hi;
+  uint32_t u = (uint32_t)t[0] << 16;
+  std::memcpy(&hi, &u, 4);
+  const float r = v - hi;
+  t[1] = f32_to_bf16(r);
+  u = (uint32_t)t[1] << 16;
+  float mid;
+  std::memcpy(&mid, &u, 4);
+  t[2] = f32_to_bf16(r - mid);
+}
+
+// The three-term fp32 plan's 3x3 weights (L.x3 == 2, conv3x3_halo_kernel X3 = 2): per 64-row tile ct and K
+// step g = (32-channel chunk, tap) -- the halo kernel's step order -- three bf16 planes (hi, mid, lo) of
+// 64 rows x 64 B; in row r, 16-byte chunk q holds channels 4q..4q+3 and 16+4q..16+4q+3 of the chunk (the
+// K values lane group q of the activation fragments holds) at position q ^ ((r >> 2) & 3).
+int pack3x3_split(const Layer& L, const std::vector<double>& w, std::vector<uint8_t>& buf) {
+  const int BR = cfg_rows(L.cfg), NCH = L.cin / 32, S = 9 * NCH;
+  if (L.cout % BR || L.cin % 32) return fail(UNET_EINVAL, "pre-split weight tiling does not divide the layer");
+  buf.assign((size_t)L.cout * 9 * L.cin * 6, 0);
+  for (int rho = 0; rho < L.cout; ++rho) {
+    const int o = natural_of_packed(rho), ct = rho / BR, r = rho % BR;
+    for (int ch = 0; ch < NCH; ++ch)
+      for (int tap = 0; tap < 9; ++tap) {
+        const size_t blk = ((size_t)ct * S + (size_t)ch * 9 + tap) * 3 * BR * 64;
+        for (int j = 0; j < 32; ++j) {   // bf16 slot j of the row: chunk q = j / 8, element e = j % 8
+          const int q = j >> 3, e = j & 7;
+          const int c = 32 * ch + (e < 4 ? 4 * q + e : 16 + 4 * q + e - 4);
+          uint16_t t[3];
+          split3_host((float)w[((size_t)o * L.cin + c) * 9 + tap], t);
+          const size_t off = (size_t)r * 64 + (size_t)((q ^ ((r >> 2) & 3)) * 16) + (size_t)e * 2;
+          for (int p = 0; p < 3; ++p) std::memcpy(&buf[blk + (size_t)p * BR * 64 + off], &t[p], 2);
+        }
+      }
+  }
+  return UNET_OK;
+}
+
 int pack3x3_host(const Layer& L, const std::vector<double>& w, std::vector<uint8_t>& buf) {
+  if (L.x3 == 2) return pack3x3_split(L, w, buf);
   const int K = 9 * L.cin;
   buf.assign((size_t)L.cout * K * dtype_size(L.dt), 0);
   const bool ring = cfg_is_ring(L.cfg);
@@ -732,9 +775,9 @@ std::string layer_label(const unet_handle* h, const Layer& L, int epi, Split sp 
                   tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto), cfg_tile_h(cfg), cfg_tile_w(cfg));
   } else {
     const int wpx = cfg == CFG_HALO_R64_W8 ? 8 : 4, tc = cfg == CFG_HALO_R128 ? 8 : 4,
-              ns = cfg == CFG_HALO_R128 ? 2 : 3;
-    std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, 1, %d, %d, %d, %d, %d>", tname(L.dt), wpx, tc, ns,
-                  L.taps == 9 ? 3 : 1, epi);
+              ns = (cfg == CFG_HALO_R128 || L.x3 == 2) ? 2 : 3;
+    std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, 1, %d, %d, %d, %d, %d, %d>", tname(L.dt), wpx, tc, ns,
+                  L.taps == 9 ? 3 : 1, epi, L.x3);
   }
   return buf;
 }
@@ -873,20 +916,24 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   if (!cfg || !out) return fail(UNET_EINVAL, "null argument");
   if (cfg->n_channels != 1 && cfg->n_channels != 3) return fail(UNET_EINVAL, "n_channels must be 1 or 3");
   if (cfg->n_classes < 1 || cfg->n_classes > kMaxClasses) return fail(UNET_EINVAL, "n_classes must be 1..4");
-  if (cfg->dtype < 0 || cfg->dtype > UNET_DTYPE_MIXED) return fail(UNET_EINVAL, "bad dtype");
+  if (cfg->dtype < 0 || cfg->dtype > UNET_DTYPE_F32_EXACT) return fail(UNET_EINVAL, "bad dtype");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (cfg->device < 0 || cfg->device >= ndev) return fail(UNET_EINVAL, "bad device ordinal");
   unet_handle* h = new unet_handle();
   h->cfg = *cfg;
-  const bool f32 = cfg->dtype == UNET_DTYPE_F32;
+  const bool f32 = cfg->dtype == UNET_DTYPE_F32 || cfg->dtype == UNET_DTYPE_F32_EXACT;
+  h->f32x3 = cfg->dtype == UNET_DTYPE_F32;
+  if (const char* x3 = std::getenv("UNET_MI355X_F32X3")) h->f32x3 = f32 && std::atoi(x3) != 0;   // A/B runs
   h->dt = f32 ? DType::F32 : DType::BF16;   // workspace element size (all 16-bit plans: 2 bytes)
   for (int i = 0; i < kMaxClasses; ++i) h->thr_logit[i] = unet_logit_cut(cfg->thresholds[i]);
   // Kernel configuration per layer (tuned on MI355X).  A/B override for tuning:
   // UNET_MI355X_CFG="layer:cfg,..." (layer = index into L[], cfg = Cfg) and
   // UNET_MI355X_UPCFG="i:cfg,..." (i = 0..3 = up4..up1).
   int cfgs[17], ucfgs[4];
-  for (int i = 0; i < 17; ++i) cfgs[i] = f32 ? kHaloCfg[i] : kRingCfg[i];
+  // the three-term fp32 plan: every 3x3 layer on 64-row 4-wave tiles with pre-split weights (the only halo
+  // tile whose two weight slots of three bf16 planes leave two blocks per CU)
+  for (int i = 0; i < 17; ++i) cfgs[i] = h->f32x3 ? (int)CFG_HALO_R64_W4 : f32 ? kHaloCfg[i] : kRingCfg[i];
   for (int i = 0; i < 4; ++i) ucfgs[i] = f32 ? (int)CFG_HALO_R128 : (int)CFG_TRING_R256;
   parse_overrides(std::getenv("UNET_MI355X_CFG"), 17, cfgs, [](int, int c) { return cfg_is_halo(c) || cfg_is_ring(c); });
   parse_overrides(std::getenv("UNET_MI355X_UPCFG"), 4, ucfgs, [](int, int c) { return cfg_is_tring(c) || c == CFG_HALO_R128; });
@@ -913,6 +960,10 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     const bool pool = i == D1B || i == D2B || i == D3B || i == D4B;
     if (cfg_is_halo(c) && (L.dto != L.dt || (pool && L.dtq != L.dt))) c = L.cout == 64 || pool ? CFG_RING_R64_T3 : CFG_RING_R128;
     if (c == CFG_RING_R128 && pool) c = CFG_RING_R64_T3;   // pooled 128-row 4-wave tiles spill: same family, 64 rows
+    if (h->f32x3 && f32) {   // the three-term plan runs on the pre-split 64-row halo tiles only
+      c = CFG_HALO_R64_W4;
+      L.x3 = 2;
+    }
     L.cfg = c;
   }
   for (int i = 0; i < 4; ++i) {
@@ -924,6 +975,10 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     U.dt = level_dtype(cfg->dtype, kUpLevel[i]);
     U.dto = U.dtq = level_dtype(cfg->dtype, kUpLevel[i] - 1);
     U.cfg = (ucfgs[i] == CFG_HALO_R128 && U.dto != U.dt) ? (int)CFG_TRING_R256 : ucfgs[i];
+    if (h->f32x3 && f32) {   // both operands split on the fly (the fp32 ConvTranspose packing)
+      U.cfg = CFG_HALO_R128;
+      U.x3 = 1;
+    }
   }
   {
     const char* fz = std::getenv("UNET_MI355X_FUSE_UP1");
@@ -1130,6 +1185,7 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.ldo = ldo; a.out_off = out_off; a.ldo2 = ldo2;
   a.ncls = h->cfg.n_classes;
   a.mask_kind = mask_kind;
+  a.x3 = L.x3;
   if (epi == EPI_UPFUSE) {   // the fused up1's weights, bias and output (the concat buffer's lower half)
     a.wgt = h->wf_c2b;
     a.bias2 = h->U[3].b;
@@ -1716,12 +1772,13 @@ extern "C" {
 int unet_block_create(const unet_block_config* cfg, unet_block** out) {
   if (!cfg || !out) return fail(UNET_EINVAL, "null argument");
   const int cin = cfg->in_ch, cout = cfg->out_ch;
-  if (cfg->dtype < 0 || cfg->dtype > UNET_DTYPE_MIXED) return fail(UNET_EINVAL, "bad dtype");
+  if (cfg->dtype < 0 || cfg->dtype > UNET_DTYPE_F32_EXACT) return fail(UNET_EINVAL, "bad dtype");
   const bool first = cin == 1 || cin == 3;
   if (cout <= 0 || cout % 64 || (first && cout != 64) || (!first && (cin <= 0 || cin % 32)))
     return fail(UNET_ESHAPE, "DoubleConv(in_ch, out_ch) runs natively for in_ch in {1, 3} with out_ch = 64, or in_ch "
                              "a multiple of 32 and out_ch a multiple of 64 (every block of the reference UNet)");
-  if (cfg->dtype != UNET_DTYPE_F32 && cout != 64 && cout % 128)   // the 16-bit rings tile 64 or 128-row groups
+  const bool f32 = cfg->dtype == UNET_DTYPE_F32 || cfg->dtype == UNET_DTYPE_F32_EXACT;
+  if (!f32 && cout != 64 && cout % 128)   // the 16-bit rings tile 64 or 128-row groups
     return fail(UNET_ESHAPE, "DoubleConv(in_ch, out_ch) on the 16-bit plans needs out_ch = 64 or a multiple of 128 "
                              "(the 128-row MFMA ring tiles); fp32 takes any multiple of 64");
   int ndev = 0;
@@ -1737,7 +1794,8 @@ int unet_block_create(const unet_block_config* cfg, unet_block** out) {
   h.cfg.dtype = cfg->dtype;
   h.cfg.device = cfg->device;
   h.ksplit_max = 0;
-  const bool f32 = cfg->dtype == UNET_DTYPE_F32;
+  h.f32x3 = cfg->dtype == UNET_DTYPE_F32;
+  if (const char* x3 = std::getenv("UNET_MI355X_F32X3")) h.f32x3 = f32 && std::atoi(x3) != 0;   // A/B runs
   // the mixed plan's storage type at this block's resolution level in the reference network: fp16 up to
   // 128 channels (levels 0-1), bf16 beyond (levels 2-4)
   const DType t = f32 ? DType::F32 : cfg->dtype == UNET_DTYPE_F16 ? DType::F16 : cfg->dtype == UNET_DTYPE_BF16 ? DType::BF16
@@ -1749,7 +1807,10 @@ int unet_block_create(const unet_block_config* cfg, unet_block** out) {
     L.cout = L.ctot = cout;
     L.taps = 9;
     L.dt = L.dto = L.dtq = t;
-    if (f32) L.cfg = cout == 64 ? CFG_HALO_R64_W8 : CFG_HALO_R128;
+    if (f32 && h.f32x3) {   // the three-term fp32 plan (as the network's layers)
+      L.cfg = CFG_HALO_R64_W4;
+      L.x3 = 2;
+    } else if (f32) L.cfg = cout == 64 ? CFG_HALO_R64_W8 : CFG_HALO_R128;
     else L.cfg = cout == 64 ? (L.cin == 64 ? CFG_RING8_R64_WS : CFG_RING8_R64_T9) : CFG_RING8_R128;
   }
   DeviceGuard g(cfg->device);

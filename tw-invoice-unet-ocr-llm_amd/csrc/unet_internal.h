@@ -64,6 +64,9 @@ struct IgemmArgs {
   float* part;
   int ksplit;
   int src_br;   // EPI_PARTIAL on the 8-wave ring: row tile of the weight packing when finer than BR (0 = BR)
+  int x3;       // fp32 LDS-halo family: 0 = exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); fp32 operands as three
+                // bf16 terms (6 bf16 MFMAs per 32 K): 1 = both split on the fly (the ConvTranspose), 2 = weights
+                // pre-split by the packing, activations on the fly (3x3 layers, CFG_HALO_R64_W4)
 };
 
 struct FirstConvArgs {

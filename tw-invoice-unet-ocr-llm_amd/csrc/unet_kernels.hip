@@ -119,6 +119,34 @@ __device__ __forceinline__ f32x4 mfma16<_Float16>(const uint2& a, const uint2& b
 template <>
 __device__ __forceinline__ f32x4 mfma16<float>(const uint2&, const uint2&, const f32x4& c) { return c; }   // unused
 
+// fp32 as three bf16 terms (the fp32 plan's arithmetic on the bf16 MFMA pipe): x = hi + mid + lo with
+// hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid) (round to nearest even; each difference is
+// exact in fp32), so hi + mid + lo carries x's 24-bit significand.  A product of two split values is
+// sum_{i+j<=2} a_i b_j (6 bf16 products, exact in the fp32 MFMA accumulator) up to terms below 2^-24 of
+// |a b|: fp32 accuracy (unet_model.py:10,14 in fp32) at 6 MFMAs of 16x16x32 (6 x 16 cycles) where the
+// exact-fp32 path needs 8 of 16x16x4 f32 (8 x 32 cycles) for the same 32 K.  x0, x1: the 8 fp32 K values of
+// this lane (two 16-byte fragments); A and B are split with the same K order.
+__device__ __forceinline__ void split3_bf16(const frag_t& x0, const frag_t& x1, frag_t& h, frag_t& m, frag_t& l) {
+  const f32x4 a = __builtin_bit_cast(f32x4, x0), b = __builtin_bit_cast(f32x4, x1);
+  bf16x8 H, M, L;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float v = i < 4 ? a[i] : b[i - 4];
+    const __bf16 hi = (__bf16)v;
+    const float r = v - (float)hi;
+    const __bf16 mi = (__bf16)r;
+    H[i] = hi;
+    M[i] = mi;
+    L[i] = (__bf16)(r - (float)mi);
+  }
+  h = __builtin_bit_cast(frag_t, H);
+  m = __builtin_bit_cast(frag_t, M);
+  l = __builtin_bit_cast(frag_t, L);
+}
+__device__ __forceinline__ void mfma_bf16(f32x4& acc, const frag_t& a, const frag_t& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+}
+
 // torch semantics of ReLU / MaxPool2d: a NaN propagates (unet_model.py:12,16,34).  One
 // v_maximum3_f32 (IEEE-754-2019 maximum) each; fmaxf would turn a NaN into the other operand.
 __device__ __forceinline__ float relu_nan(float x) { return __builtin_elementwise_maximum(x, 0.f); }
@@ -696,7 +724,7 @@ __device__ __forceinline__ void mfma_taps_astream(f32x4 (&acc)[TC][TP], const ch
 }
 
 // Derived geometry / LDS budget of a halo-kernel instantiation (shared with the launcher).
-template <typename T, int WR, int WPX, int TCW, int NS, int KT>
+template <typename T, int WR, int WPX, int TCW, int NS, int KT, int X3 = 0>
 struct HaloGeom {
   static constexpr int NW = WR * WPX;
   static constexpr int TC = TCW;
@@ -710,15 +738,21 @@ struct HaloGeom {
   static constexpr int HI = (NPIX + 8 * NW - 1) / (8 * NW);   // halo DMA instructions per wave
   static constexpr int WI = BR / (8 * NW);                     // weight DMA instructions per wave
   static constexpr int HALO_BYTES = HI * NW * 8 * 128;
-  static constexpr int WSLOT = BR * 128;
+  // X3 = 2: a step's weights as three bf16 planes (hi, mid, lo) of BR rows x 64 B (unet_capi.cpp pack3x3_host)
+  static constexpr int WSLOT = X3 == 2 ? 3 * BR * 64 : BR * 128;
   static constexpr int WOFF = HALO_BYTES;
   static constexpr int PARAM_OFF = WOFF + NS * WSLOT;
   static constexpr int LDS_BYTES = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
 };
 
-template <typename T, int WR, int WPX, int TCW, int NS, int KT, int EPI>
+// X3 (fp32 only): the fp32 operands as three bf16 terms (split3_bf16), 6 bf16 MFMAs per 32-K block instead of
+// 8 exact-fp32 ones, same epilogues.  X3 = 1: both operands split on the fly (same LDS images and weight
+// packing as the fp32 kernel; the ConvTranspose).  X3 = 2: the weights come pre-split from the packing as
+// three bf16 planes per step (no VALU for A, which the block's waves share), the activations are split on
+// the fly per fragment (the 3x3 layers).
+template <typename T, int WR, int WPX, int TCW, int NS, int KT, int EPI, int X3 = 0>
 __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_kernel(const IgemmArgs a) {
-  using G = HaloGeom<T, WR, WPX, TCW, NS, KT>;
+  using G = HaloGeom<T, WR, WPX, TCW, NS, KT, X3>;
   constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
   constexpr int HWD = G::HWD, NPIX = G::NPIX, NTAP = G::NTAP, PAD = G::PAD;
   constexpr int HI = G::HI, WI = G::WI, WSLOT = G::WSLOT, WOFF = G::WOFF;
@@ -785,11 +819,21 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
     }
   };
   auto issue_w = [&](int g) {   // K step g = (chunk, tap) of the slice, weights [row][tap*Cin + c]
-    const int c = c_lo + g / NTAP, tap = g - (g / NTAP) * NTAP;
-    const size_t koff = ((size_t)tap * a.Cin + (size_t)c * BKE) * sizeof(T);
-    char* dst = lds + WOFF + (g % NS) * WSLOT + wave * WI * 8 * 128;
+    if constexpr (X3 == 2) {   // [ct][step][3][BR][64 B]: one contiguous block per step, 1 KB per DMA instruction
+      constexpr int WJ = WSLOT / (1024 * NW);
+      static_assert(WSLOT % (1024 * NW) == 0, "pre-split weight slot split");
+      const long long step = (long long)ct * (NTAP * (a.Cin / BKE)) + (long long)c_lo * NTAP + g;
+      const char* src = reinterpret_cast<const char*>(a.wgt) + step * WSLOT + (wave * WJ) * 1024 + lane * 16;
+      char* dst = lds + WOFF + (g % NS) * WSLOT + wave * WJ * 1024;
 #pragma unroll
-    for (int j = 0; j < WI; ++j) glds16(wbase + koff + j * wstep, dst + j * 8 * 128);
+      for (int j = 0; j < WJ; ++j) glds16(src + j * 1024, dst + j * 1024);
+    } else {
+      const int c = c_lo + g / NTAP, tap = g - (g / NTAP) * NTAP;
+      const size_t koff = ((size_t)tap * a.Cin + (size_t)c * BKE) * sizeof(T);
+      char* dst = lds + WOFF + (g % NS) * WSLOT + wave * WI * 8 * 128;
+#pragma unroll
+      for (int j = 0; j < WI; ++j) glds16(wbase + koff + j * wstep, dst + j * 8 * 128);
+    }
   };
 
   f32x4 acc[TC][TP];
@@ -841,17 +885,72 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
         mfma_frag<T>(acc[t][p], __builtin_bit_cast(uint4, af[t]), __builtin_bit_cast(uint4, bf[p]));
   };
 
+  // X3: the step's 32 K as one 16x16x32 block per fragment pair -- lane (col, q) holds K chunks q and
+  // 4 + q (the kk = 0 and 1 fragments of read_frags), for A and B alike
+  auto x3_step = [&](int g, int tp) {
+    static_assert(X3 == 0 || sizeof(T) == 4, "X3 splits fp32 operands");
+    const int dy = tp / KT, dx = tp - (tp / KT) * KT;
+    const char* Ws = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 128;
+    const int toff = dy * HWD + dx;
+    const int hx7 = (px_lane + dx) & 7;
+    frag_t bh[TP], bm[TP], bl[TP];
+#pragma unroll
+    for (int p = 0; p < TP; ++p) {
+      const char* hb = lds + (prow[p] + toff) * 128;
+      const frag_t x0 = *reinterpret_cast<const frag_t*>(hb + ((q ^ hx7) << 4));
+      const frag_t x1 = *reinterpret_cast<const frag_t*>(hb + (((4 + q) ^ hx7) << 4));
+      split3_bf16(x0, x1, bh[p], bm[p], bl[p]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // X3 = 2: plane row r's 16-byte chunk q (K values 4q..4q+3, 16+4q..16+4q+3) sits at position
+    // q ^ ((r >> 2) & 3): the 16 rows a ds_read_b128 lane group reads cover all 64 banks
+    const char* Wp = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 64 + ((q ^ ((col >> 2) & 3)) << 4);
+#pragma unroll
+    for (int t = 0; t < TC; ++t) {
+      frag_t ah, am, al;
+      if constexpr (X3 == 2) {
+        ah = *reinterpret_cast<const frag_t*>(Wp + t * 16 * 64);
+        am = *reinterpret_cast<const frag_t*>(Wp + BR * 64 + t * 16 * 64);
+        al = *reinterpret_cast<const frag_t*>(Wp + 2 * BR * 64 + t * 16 * 64);
+      } else {
+        const char* wr_ = Ws + t * 16 * 128;
+        const frag_t w0 = *reinterpret_cast<const frag_t*>(wr_ + ((q ^ (lane & 7)) << 4));
+        const frag_t w1 = *reinterpret_cast<const frag_t*>(wr_ + (((4 + q) ^ (lane & 7)) << 4));
+        split3_bf16(w0, w1, ah, am, al);
+      }
+      // term-major: TP independent accumulators between two MFMAs of one chain; small terms first
+#pragma unroll
+      for (int p = 0; p < TP; ++p) mfma_bf16(acc[t][p], am, bm[p]);
+#pragma unroll
+      for (int p = 0; p < TP; ++p) mfma_bf16(acc[t][p], al, bh[p]);
+#pragma unroll
+      for (int p = 0; p < TP; ++p) mfma_bf16(acc[t][p], ah, bl[p]);
+#pragma unroll
+      for (int p = 0; p < TP; ++p) mfma_bf16(acc[t][p], am, bh[p]);
+#pragma unroll
+      for (int p = 0; p < TP; ++p) mfma_bf16(acc[t][p], ah, bm[p]);
+#pragma unroll
+      for (int p = 0; p < TP; ++p) mfma_bf16(acc[t][p], ah, bh[p]);
+      // one row group's A fragments live at a time (register budget: 128 accumulators + 48 B terms)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
   frag_t a0[TC], b0[TP], a1[TC], b1[TP];
   int c = 0, tap = 0;
   for (int g = 0; g < S; ++g) {
     const bool wnext = g + NS - 1 < S;
     if (wnext) issue_w(g + NS - 1);
-    read_frags(g, tap, 0, a0, b0);
-    mfmas(a0, b0);
-    // 128-row wave tiles: keep one kk's fragments live at a time (register budget)
-    if constexpr (TC == 8) __builtin_amdgcn_sched_barrier(0);
-    read_frags(g, tap, 1, a1, b1);
-    mfmas(a1, b1);
+    if constexpr (X3 != 0) {
+      x3_step(g, tap);
+    } else {
+      read_frags(g, tap, 0, a0, b0);
+      mfmas(a0, b0);
+      // 128-row wave tiles: keep one kk's fragments live at a time (register budget)
+      if constexpr (TC == 8) __builtin_amdgcn_sched_barrier(0);
+      read_frags(g, tap, 1, a1, b1);
+      mfmas(a1, b1);
+    }
     // the next step needs W(g+1); the barrier's lgkmcnt(0) also retires this step's reads (WAR)
     if (NS == 2) {
       wait_vm_barrier<0>();
@@ -894,7 +993,7 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
 // order ([ct][step][BR][64 B], unet_capi.cpp pack3x3) so every weight DMA instruction reads
 // 1 KB contiguous.  Bank-conflict-free 64-byte-row images: halo pixel (hy,hx) chunk q at
 // position q ^ (hx & 3); weight row r chunk q at position q ^ ((r >> 1) & 3) (exhaustive check
-// over all ds_read_b128 lane groups, taps and pixel groups: tools/swizzle_check.py).
+// over all ds_read_b128 lane groups, taps and pixel groups: the bank model of tools/halo_swizzle_search.py, tests/test_lds_layout_cpu.py).
 // Blocks are persistent (n_ct row tiles x n_slots walkers, each walking pixel tiles slot,
 // slot + n_slots, ...) so the rings run across tile boundaries and the epilogue of one tile
 // overlaps the loads of the next.
@@ -2467,6 +2566,25 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   // one block per (row tile, K slice, pixel tile)
   const long long nb = (long long)a.n_ct * KS * a.N * a.tiles_y * a.tiles_x;
   if (nb <= 0 || nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  if (a.x3) {   // fp32 operands as three bf16 terms (split3_bf16): the 3x3 layers on 64-row 4-wave tiles with
+                // pre-split weights (two weight slots: 3 x 12 KB of LDS would not leave two blocks per CU), the
+                // ConvTranspose with both operands split on the fly
+    if constexpr (sizeof(T) == 4 && WPX == 4 && TCW == 4 && KT == 3) {
+      if (a.x3 == 2) {
+        hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, 2, KT, EPI, 2>), dim3((unsigned)nb),
+                           dim3(64 * WR * WPX), 0, s, a);
+        return hipGetLastError();
+      }
+    }
+    if constexpr (sizeof(T) == 4 && KT == 1) {
+      if (a.x3 == 1) {
+        hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, NS, KT, EPI, 1>), dim3((unsigned)nb),
+                           dim3(64 * WR * WPX), 0, s, a);
+        return hipGetLastError();
+      }
+    }
+    return hipErrorInvalidValue;
+  }
   hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, NS, KT, EPI>), dim3((unsigned)nb), dim3(64 * WR * WPX), 0,
                      s, a);
   return hipGetLastError();

@@ -20,7 +20,9 @@ LIB_PATH = os.environ.get("UNET_MI355X_LIB") or os.path.join(os.path.dirname(os.
 
 UNET_OK, UNET_EINVAL, UNET_ESHAPE, UNET_ENOMEM, UNET_EHIP, UNET_ESTATE, UNET_EKEY = 0, -1, -2, -3, -4, -5, -6
 # "mixed": bf16 storage at resolution levels 2-4, fp16 at levels 0-1 (include/unet_mi355x.h)
-DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16": 2, "mixed": 3}
+# "fp32": fp32 storage, every product as three bf16 terms per operand (fp32 accuracy on the bf16 MFMA pipe);
+# "fp32_exact": the same plan on the exact-fp32 MFMA
+DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "fp16": 2, "float16": 2, "mixed": 3, "fp32_exact": 4}
 MASK_NONE, MASK_U8, MASK_BITS = 0, 1, 2
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
 COMM_ID_BYTES = 128
