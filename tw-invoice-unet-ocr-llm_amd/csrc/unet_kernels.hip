@@ -735,11 +735,14 @@ struct HaloGeom {
   static constexpr int HWD = 16 + 2 * PAD;          // halo width = height
   static constexpr int NPIX = HWD * HWD;
   static constexpr int NTAP = KT * KT;
-  static constexpr int HI = (NPIX + 8 * NW - 1) / (8 * NW);   // halo DMA instructions per wave
-  static constexpr int WI = BR / (8 * NW);                     // weight DMA instructions per wave
-  static constexpr int HALO_BYTES = HI * NW * 8 * 128;
-  // X3 = 2: a step's weights as three bf16 planes (hi, mid, lo) of BR rows x 64 B (unet_capi.cpp pack3x3_host)
+  static constexpr int HI = (NPIX + 8 * NW - 1) / (8 * NW);   // halo DMA instructions per wave (at most)
+  // X3 = 2: a step's weights as three bf16 planes (hi, mid, lo) of BR rows x 64 B (unet_capi.cpp pack3x3_host);
+  // the halo's 1 KB DMA pieces are dealt over the waves round-robin, only as many as the halo needs (NI),
+  // so that three weight slots fit beside it at two blocks per CU
   static constexpr int WSLOT = X3 == 2 ? 3 * BR * 64 : BR * 128;
+  static constexpr int WI = X3 == 2 ? WSLOT / (1024 * NW) : BR / (8 * NW);   // weight DMA instructions per wave
+  static constexpr int NI = (NPIX + 7) / 8;                    // halo DMA pieces (X3 = 2)
+  static constexpr int HALO_BYTES = X3 == 2 ? NI * 1024 : HI * NW * 8 * 128;
   static constexpr int WOFF = HALO_BYTES;
   static constexpr int PARAM_OFF = WOFF + NS * WSLOT;
   static constexpr int LDS_BYTES = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
@@ -808,7 +811,10 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
     const long long c0 = (long long)c * BKE;
 #pragma unroll
     for (int j = 0; j < HI; ++j) {
-      const int row = (wave * HI + j) * 8 + (lane >> 3);
+      const int piece = X3 == 2 ? j * NW + wave : wave * HI + j;   // X3 = 2: round-robin, NI pieces in all
+      if (X3 == 2 && piece >= G::NI) break;
+      if constexpr (X3 == 2) dst = lds + (piece - j) * 1024;       // + j KB below
+      const int row = piece * 8 + (lane >> 3);
       const int hy = row / HWD, hx = row - hy * HWD;
       const int iy = ty * 16 + hy - PAD, ix = tx * 16 + hx - PAD;
       const bool ok = row < NPIX && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
@@ -820,7 +826,7 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
   };
   auto issue_w = [&](int g) {   // K step g = (chunk, tap) of the slice, weights [row][tap*Cin + c]
     if constexpr (X3 == 2) {   // [ct][step][3][BR][64 B]: one contiguous block per step, 1 KB per DMA instruction
-      constexpr int WJ = WSLOT / (1024 * NW);
+      constexpr int WJ = WI;
       static_assert(WSLOT % (1024 * NW) == 0, "pre-split weight slot split");
       const long long step = (long long)ct * (NTAP * (a.Cin / BKE)) + (long long)c_lo * NTAP + g;
       const char* src = reinterpret_cast<const char*>(a.wgt) + step * WSLOT + (wave * WJ) * 1024 + lane * 16;
@@ -2567,11 +2573,11 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   const long long nb = (long long)a.n_ct * KS * a.N * a.tiles_y * a.tiles_x;
   if (nb <= 0 || nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
   if (a.x3) {   // fp32 operands as three bf16 terms (split3_bf16): the 3x3 layers on 64-row 4-wave tiles with
-                // pre-split weights (two weight slots: 3 x 12 KB of LDS would not leave two blocks per CU), the
+                // pre-split weights (three weight slots beside an exactly sized halo: 78 KB), the
                 // ConvTranspose with both operands split on the fly
     if constexpr (sizeof(T) == 4 && WPX == 4 && TCW == 4 && KT == 3) {
       if (a.x3 == 2) {
-        hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, 2, KT, EPI, 2>), dim3((unsigned)nb),
+        hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, 3, KT, EPI, 2>), dim3((unsigned)nb),
                            dim3(64 * WR * WPX), 0, s, a);
         return hipGetLastError();
       }
