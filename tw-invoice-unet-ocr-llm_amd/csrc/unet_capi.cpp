@@ -463,7 +463,7 @@ void split3_host(float v, uint16_t (&t)[3]) {
 // The three-term fp32 plan's 3x3 weights (L.x3 == 2, conv3x3_halo_kernel X3 = 2): per 64-row tile ct and K
 // step g = (32-channel chunk, tap) -- the halo kernel's step order -- three bf16 planes (hi, mid, lo) of
 // 64 rows x 64 B; in row r, 16-byte chunk q holds channels 4q..4q+3 and 16+4q..16+4q+3 of the chunk (the
-// K values lane group q of the activation fragments holds) at position q ^ ((r >> 2) & 3).
+// K values lane group q of the activation fragments holds) at position q ^ ((r >> 1) & 3).
 int pack3x3_split(const Layer& L, const std::vector<double>& w, std::vector<uint8_t>& buf) {
   const int BR = cfg_rows(L.cfg), NCH = L.cin / 32, S = 9 * NCH;
   if (L.cout % BR || L.cin % 32) return fail(UNET_EINVAL, "pre-split weight tiling does not divide the layer");
@@ -478,7 +478,7 @@ int pack3x3_split(const Layer& L, const std::vector<double>& w, std::vector<uint
           const int c = 32 * ch + (e < 4 ? 4 * q + e : 16 + 4 * q + e - 4);
           uint16_t t[3];
           split3_host((float)w[((size_t)o * L.cin + c) * 9 + tap], t);
-          const size_t off = (size_t)r * 64 + (size_t)((q ^ ((r >> 2) & 3)) * 16) + (size_t)e * 2;
+          const size_t off = (size_t)r * 64 + (size_t)((q ^ ((r >> 1) & 3)) * 16) + (size_t)e * 2;
           for (int p = 0; p < 3; ++p) std::memcpy(&buf[blk + (size_t)p * BR * 64 + off], &t[p], 2);
         }
       }

@@ -909,8 +909,9 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
       __builtin_amdgcn_sched_barrier(0);
     }
     // X3 = 2: plane row r's 16-byte chunk q (K values 4q..4q+3, 16+4q..16+4q+3) sits at position
-    // q ^ ((r >> 2) & 3): the 16 rows a ds_read_b128 lane group reads cover all 64 banks
-    const char* Wp = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 64 + ((q ^ ((col >> 2) & 3)) << 4);
+    // q ^ ((r >> 1) & 3): each ds_read_b128 lane group's 16 pieces cover the 64 banks once (MI355X_MICROARCH.md
+    // §LDS lane groups; checked in tests/test_lds_layout_cpu.py)
+    const char* Wp = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 64 + ((q ^ ((col >> 1) & 3)) << 4);
 #pragma unroll
     for (int t = 0; t < TC; ++t) {
       frag_t ah, am, al;
@@ -2573,11 +2574,12 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   const long long nb = (long long)a.n_ct * KS * a.N * a.tiles_y * a.tiles_x;
   if (nb <= 0 || nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
   if (a.x3) {   // fp32 operands as three bf16 terms (split3_bf16): the 3x3 layers on 64-row 4-wave tiles with
-                // pre-split weights (three weight slots beside an exactly sized halo: 78 KB), the
+                // pre-split weights (two weight slots: a third beside the exactly sized halo fits, 78 KB, but
+                // measured 2 % slower), the
                 // ConvTranspose with both operands split on the fly
     if constexpr (sizeof(T) == 4 && WPX == 4 && TCW == 4 && KT == 3) {
       if (a.x3 == 2) {
-        hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, 3, KT, EPI, 2>), dim3((unsigned)nb),
+        hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, 2, KT, EPI, 2>), dim3((unsigned)nb),
                            dim3(64 * WR * WPX), 0, s, a);
         return hipGetLastError();
       }
