@@ -1264,8 +1264,8 @@ def test_run_unet_masks_survive_later_calls():
                 assert np.array_equal(again[k], snap[k]), (j, k)
         st = inf._staging[str(inf.DEVICE)]
         assert len(st.masks.blocks) == inf._Staging.MASK_POOL
-        # one photo graph per geometry, its masks copy retargeted to each block lent
-        assert len(st.graphs) == 1 and st.retarget
+        # one photo graph per geometry (three photos), its masks copy retargeted to each block lent
+        assert len(st.graphs) == len({(p.size, p.mode) for p in photos}) and st.retarget
         del kept, masks, again
         import gc
         gc.collect()

@@ -271,10 +271,12 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
   // candidate row tiles: the layer's own; on the ring also 64-row halves (twice the blocks per slice, so
   // half the slices for the same CU count; 0.8x the per-CU rate: half the MFMAs per halo byte)
   const int own = cfg_rows(L.cfg);
-  double tbest = flops / ((double)std::min<long long>(tiles * (L.ctot / own), 256) * (ring8 ? 6e12 : 0.5e12));
+  // the LDS-halo family's per-CU rate: exact-fp32 MFMA ~0.5 TF/s, the three-term plan ~0.85 TF/s (fp32 FLOPs)
+  const double halo_rate = L.x3 ? 0.85e12 : 0.5e12;
+  double tbest = flops / ((double)std::min<long long>(tiles * (L.ctot / own), 256) * (ring8 ? 6e12 : halo_rate));
   for (int rows : {own, ring8 ? 64 : 0}) {
     if (rows == 0) break;
-    const double rate = ring8 ? (rows == 128 ? 6e12 : 4.8e12) : 0.5e12;
+    const double rate = ring8 ? (rows == 128 ? 6e12 : 4.8e12) : halo_rate;
     const long long blocks = tiles * (L.ctot / rows);
     if (forced > 0) {   // A/B runs: ks on the layer's own row tile, ks + 100 on 64-row tiles (the ring)
       const int fks = forced % 100, frows = forced >= 100 ? 64 : own;
@@ -478,7 +480,7 @@ int pack3x3_split(const Layer& L, const std::vector<double>& w, std::vector<uint
           const int c = 32 * ch + (e < 4 ? 4 * q + e : 16 + 4 * q + e - 4);
           uint16_t t[3];
           split3_host((float)w[((size_t)o * L.cin + c) * 9 + tap], t);
-          const size_t off = (size_t)r * 64 + (size_t)((q ^ ((r >> 1) & 3)) * 16) + (size_t)e * 2;
+          const size_t off = (size_t)r * 64 + (size_t)((q ^ ((r >> UNET_X3_SWZ) & 3)) * 16) + (size_t)e * 2;
           for (int p = 0; p < 3; ++p) std::memcpy(&buf[blk + (size_t)p * BR * 64 + off], &t[p], 2);
         }
       }
