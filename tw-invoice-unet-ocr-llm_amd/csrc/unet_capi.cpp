@@ -777,7 +777,7 @@ std::string layer_label(const unet_handle* h, const Layer& L, int epi, Split sp 
                   tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto), cfg_tile_h(cfg), cfg_tile_w(cfg));
   } else {
     const int wpx = cfg == CFG_HALO_R64_W8 ? 8 : 4, tc = cfg == CFG_HALO_R128 ? 8 : 4,
-              ns = cfg == CFG_HALO_R128 ? 2 : 3;
+              ns = L.x3 == 2 ? UNET_X3_NS : cfg == CFG_HALO_R128 ? 2 : 3;
     std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, 1, %d, %d, %d, %d, %d, %d>", tname(L.dt), wpx, tc, ns,
                   L.taps == 9 ? 3 : 1, epi, L.x3);
   }
