@@ -480,7 +480,7 @@ int pack3x3_split(const Layer& L, const std::vector<double>& w, std::vector<uint
           const int c = 32 * ch + (e < 4 ? 4 * q + e : 16 + 4 * q + e - 4);
           uint16_t t[3];
           split3_host((float)w[((size_t)o * L.cin + c) * 9 + tap], t);
-          const size_t off = (size_t)r * 64 + (size_t)((q ^ ((r >> UNET_X3_SWZ) & 3)) * 16) + (size_t)e * 2;
+          const size_t off = (size_t)r * 64 + (size_t)((q ^ ((r >> 1) & 3)) * 16) + (size_t)e * 2;
           for (int p = 0; p < 3; ++p) std::memcpy(&buf[blk + (size_t)p * BR * 64 + off], &t[p], 2);
         }
       }
@@ -777,7 +777,7 @@ std::string layer_label(const unet_handle* h, const Layer& L, int epi, Split sp 
                   tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto), cfg_tile_h(cfg), cfg_tile_w(cfg));
   } else {
     const int wpx = cfg == CFG_HALO_R64_W8 ? 8 : 4, tc = cfg == CFG_HALO_R128 ? 8 : 4,
-              ns = L.x3 == 2 ? UNET_X3_NS : cfg == CFG_HALO_R128 ? 2 : 3;
+              ns = L.x3 == 2 ? 2 : cfg == CFG_HALO_R128 ? 2 : 3;
     std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, 1, %d, %d, %d, %d, %d, %d>", tname(L.dt), wpx, tc, ns,
                   L.taps == 9 ? 3 : 1, epi, L.x3);
   }

@@ -9,23 +9,6 @@ namespace unet {
 
 enum class DType : int { F32 = 0, BF16 = 1, F16 = 2 };
 
-// Three-term fp32 plan, timing-only A/B builds (make EXTRA=-D...; the product uses the defaults): the shift of
-// the pre-split weight planes' chunk swizzle (position q ^ ((r >> UNET_X3_SWZ) & 3)) and the pixel-group-major
-// pipelined step (1) vs the row-group-major one (0).
-#ifndef UNET_X3_SWZ
-#define UNET_X3_SWZ 1
-#endif
-#ifndef UNET_X3_PIPE
-#define UNET_X3_PIPE 1
-#endif
-// ... the next step's first activation split carried under this step's last MFMAs (1), and the weight slots (2 or 3)
-#ifndef UNET_X3_CARRY
-#define UNET_X3_CARRY 1
-#endif
-#ifndef UNET_X3_NS
-#define UNET_X3_NS 2
-#endif
-
 inline size_t dtype_size(DType t) { return t == DType::F32 ? 4 : 2; }
 
 // Epilogue kinds of the implicit-GEMM kernel.

@@ -893,22 +893,19 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
 
   // X3: the step's 32 K as one 16x16x32 block per fragment pair -- lane (col, q) holds K chunks q and
   // 4 + q (the kk = 0 and 1 fragments of read_frags), for A and B alike
-  frag_t x3_ch, x3_cm, x3_cl;   // X3 = 2: the next step's group-0 activation terms, split under this step
-  bool x3_carried = false;
   auto x3_step = [&](int g, int tp) {
     static_assert(X3 == 0 || sizeof(T) == 4, "X3 splits fp32 operands");
     const int dy = tp / KT, dx = tp - (tp / KT) * KT;
     const char* Ws = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 128;
     const int toff = dy * HWD + dx;
     const int hx7 = (px_lane + dx) & 7;
-    if constexpr (X3 == 2 && UNET_X3_PIPE) {
+    if constexpr (X3 == 2) {
       // pixel-group-major: the step's A terms (3 x TC fragments, pre-split) stay in registers, and the split
       // of group p + 1's activations (VALU) is interleaved with group p's 6 x TC MFMAs, so the VALU runs
-      // under the matrix pipe instead of in a block in front of it.  The last group's MFMAs carry the split of
-      // the NEXT step's group 0 when that step reads the same halo chunk (taps 0..7 of 9), so only a chunk's
-      // first step opens with an exposed split.  Same products, same per-accumulator order (small terms first)
-      // as the row-group-major order below.
-      const char* Wp = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 64 + ((q ^ ((col >> UNET_X3_SWZ) & 3)) << 4);
+      // under the matrix pipe instead of in a block in front of it (-6.5 % against the row-group-major order
+      // below on the same box; carrying the next step's group-0 split under the last group's MFMAs measured
+      // +1.5 %).  Same products, same per-accumulator order (small terms first) as the row-group-major order.
+      const char* Wp = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 64 + ((q ^ ((col >> 1) & 3)) << 4);
       frag_t ah[TC], am[TC], al[TC];
 #pragma unroll
       for (int t = 0; t < TC; ++t) {
@@ -921,19 +918,10 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
         v0 = *reinterpret_cast<const frag_t*>(hb + ((q ^ h7) << 4));
         v1 = *reinterpret_cast<const frag_t*>(hb + (((4 + q) ^ h7) << 4));
       };
-      const bool carry_next = UNET_X3_CARRY && tp + 1 < NTAP;   // the next step's tap reads this halo chunk too
-      const int tn = tp + 1, dyn = tn / KT, dxn = tn - (tn / KT) * KT;
-      const int toffn = dyn * HWD + dxn, hx7n = (px_lane + dxn) & 7;
       frag_t bh, bm, bl, x0, x1;
-      if (x3_carried) {
-        bh = x3_ch;
-        bm = x3_cm;
-        bl = x3_cl;
-      } else {
-        braw(0, toff, hx7, x0, x1);
-        split3_bf16(x0, x1, bh, bm, bl);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      braw(0, toff, hx7, x0, x1);
+      split3_bf16(x0, x1, bh, bm, bl);
+      __builtin_amdgcn_sched_barrier(0);
       auto group = [&](int p, bool split_next) {
         frag_t nh, nm, nl;
 #pragma unroll
@@ -968,16 +956,7 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
         braw(p + 1, toff, hx7, x0, x1);
         group(p, true);
       }
-      if (carry_next) {
-        braw(0, toffn, hx7n, x0, x1);
-        group(TP - 1, true);
-        x3_ch = bh;
-        x3_cm = bm;
-        x3_cl = bl;
-      } else {
-        group(TP - 1, false);
-      }
-      x3_carried = carry_next;
+      group(TP - 1, false);
       return;
     }
     frag_t bh[TP], bm[TP], bl[TP];
@@ -992,7 +971,7 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
     // X3 = 2: plane row r's 16-byte chunk q (K values 4q..4q+3, 16+4q..16+4q+3) sits at position
     // q ^ ((r >> 1) & 3): each ds_read_b128 lane group's 16 pieces cover the 64 banks once (MI355X_MICROARCH.md
     // §LDS lane groups; checked in tests/test_lds_layout_cpu.py)
-    const char* Wp = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 64 + ((q ^ ((col >> UNET_X3_SWZ) & 3)) << 4);
+    const char* Wp = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 64 + ((q ^ ((col >> 1) & 3)) << 4);
 #pragma unroll
     for (int t = 0; t < TC; ++t) {
       frag_t ah, am, al;
@@ -2660,7 +2639,7 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
                 // ConvTranspose with both operands split on the fly
     if constexpr (sizeof(T) == 4 && WPX == 4 && TCW == 4 && KT == 3) {
       if (a.x3 == 2) {
-        hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, UNET_X3_NS, KT, EPI, 2>), dim3((unsigned)nb),
+        hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, 2, KT, EPI, 2>), dim3((unsigned)nb),
                            dim3(64 * WR * WPX), 0, s, a);
         return hipGetLastError();
       }
