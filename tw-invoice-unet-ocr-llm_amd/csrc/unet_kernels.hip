@@ -127,6 +127,12 @@ __device__ __forceinline__ f32x4 mfma16<float>(const uint2&, const uint2&, const
 // exact-fp32 path needs 8 of 16x16x4 f32 (8 x 32 cycles) for the same 32 K.  x0, x1: the 8 fp32 K values of
 // this lane (two 16-byte fragments); A and B are split with the same K order.
 __device__ __forceinline__ void split3_bf16(const frag_t& x0, const frag_t& x1, frag_t& h, frag_t& m, frag_t& l) {
+#ifdef UNET_ABL_X3_NOSPLIT   // timing-only ablation build: no split arithmetic (operand bits reused as terms)
+  h = x0;
+  m = x1;
+  l = x0;
+  return;
+#endif
   const f32x4 a = __builtin_bit_cast(f32x4, x0), b = __builtin_bit_cast(f32x4, x1);
   bf16x8 H, M, L;
 #pragma unroll
@@ -1025,8 +1031,13 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
       if (wnext) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
     }
     if (tap == NTAP - 1 && c + 1 < nch) {   // every wave has finished reading the halo (barrier above)
-      issue_halo(c_lo + c + 1);
-      wait_vm_barrier<0>();
+#ifdef UNET_ABL_X3_NOHALO   // timing-only ablation build: the chunk's halo is never reloaded
+      if constexpr (X3 == 0)
+#endif
+      {
+        issue_halo(c_lo + c + 1);
+        wait_vm_barrier<0>();
+      }
     }
     if (++tap == NTAP) { tap = 0; ++c; }
   }
