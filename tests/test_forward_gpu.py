@@ -1265,11 +1265,39 @@ def test_run_unet_masks_survive_later_calls():
         st = inf._staging[str(inf.DEVICE)]
         assert len(st.masks.blocks) == inf._Staging.MASK_POOL
         # one photo graph per geometry (three photos), its masks copy retargeted to each block lent
-        assert len(st.graphs) == len({(p.size, p.mode) for p in photos}) and st.retarget
+        assert len(st.graphs) == len({(p.size, p.mode) for p in photos}) and st.retarget_error is None, st.retarget_error
         del kept, masks, again
         import gc
         gc.collect()
         assert all(st.masks.idle)   # every returned mask dropped: every block is free again
+
+
+def test_photo_graph_retargets_between_blocks_and_the_shared_buffer():
+    """One photo geometry, one graph: its masks copy is retargeted (unet_photo_graph_set_masks) from a lent
+    pinned block to the shared pinned buffer (every block held: run_unet copies out of it) and back, and
+    every call returns the same masks and crops."""
+    import gc
+    from unet_mi355x import inference as inf
+    photo = _photos(1)[0]
+    with tempfile.TemporaryDirectory() as td:
+        ck = _save_ckpt(td)
+        inf.DEVICE = DEV
+        first = inf.run_unet(photo, ck, compute_dtype="mixed")
+        first = ({k: v.copy() for k, v in first[0].items()}, first[1])
+        gc.collect()
+        st = inf._staging[str(inf.DEVICE)]
+        st.drop_graphs()
+        st.retarget_error = None
+        held = [inf.run_unet(photo, ck, compute_dtype="mixed") for _ in range(inf._Staging.MASK_POOL + 2)]
+        assert not any(st.masks.idle)                     # every block lent: the last calls used the shared buffer
+        for r in held:
+            _same_result(r, first, inf.FIELDS)
+        del held, r
+        gc.collect()
+        again = inf.run_unet(photo, ck, compute_dtype="mixed")   # back onto a block
+        _same_result(again, first, inf.FIELDS)
+        assert len(st.graphs) == 1
+        assert st.retarget_error is None, st.retarget_error
 
 
 def test_photo_graph_eviction_beside_batch_calls_on_another_thread():
@@ -1307,7 +1335,7 @@ def test_photo_graph_eviction_beside_batch_calls_on_another_thread():
             for r in range(12):
                 i = r % len(singles)
                 _same_result(inf.run_unet(singles[i], ck, compute_dtype="mixed"), want_single[i], inf.FIELDS)
-                assert len(st.graphs) == 1
+                assert len(st.graphs) == 1, (len(st.graphs), st.retarget_error)
         finally:
             stop.set()
             th.join(120)

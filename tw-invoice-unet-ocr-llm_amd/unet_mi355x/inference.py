@@ -259,7 +259,7 @@ class _Staging:
         self.hm, self.hb, self.hr, self.hs = self._outputs(torch.empty(self._out_bytes(), dtype=torch.uint8, pin_memory=True))
         self.graphs: OrderedDict = OrderedDict()   # key -> (model, native.Graph); key = (ih, iw, c)
         self.masks = _MaskPool(self.m.shape[1:], self.MASK_POOL)
-        self.retarget = True   # False: this HIP runtime refused to retarget a masks copy; one graph per target
+        self.retarget_error = None   # the runtime's last refusal to retarget a masks copy (then: re-capture)
 
     @staticmethod
     def _out_bytes():
@@ -320,26 +320,29 @@ class _Staging:
         if e is not None:
             e[1].close()
 
-    def graph_key(self, img: torch.Tensor, target: torch.Tensor):
-        return tuple(img.shape) if self.retarget else (tuple(img.shape), target.data_ptr())
+    def graph_key(self, img: torch.Tensor, target: torch.Tensor = None):
+        return tuple(img.shape)
 
     def photo_graph(self, model, img: torch.Tensor, target: torch.Tensor):
         """The photo graph of (model, photo geometry): upload + resize + forward (masks, boxes) + crop
         statistics + copies back (unet_photo_graph_create), captured at the first call of the geometry, its
-        masks copy pointed at ``target`` (a lent mask block, or the shared pinned buffer)."""
-        key = self.graph_key(img, target)
+        masks copy pointed at ``target`` (a lent mask block, or the shared pinned buffer).  A cached graph is
+        retargeted (unet_photo_graph_set_masks); should the runtime refuse that, the geometry's graph is
+        captured again over the new target (the refusal is kept in ``retarget_error``)."""
+        key = self.graph_key(img)
         e = self.graphs.get(key)
         if e is not None and e[0] is model:
-            self.graphs.move_to_end(key)
             g = e[1]
-            if self.retarget and g.masks_ptr != target.data_ptr():
+            if g.masks_ptr != target.data_ptr():
                 try:
                     g.set_masks(target.view(self.hm.shape))
-                except RuntimeError:   # this runtime cannot retarget a captured copy: one graph per target
-                    self.retarget = False
-                    self.drop_graphs()
-                    return self.photo_graph(model, img, target)
-            return g
+                except RuntimeError as exc:
+                    self.retarget_error = str(exc)
+                    self.drop_graph(key)
+                    e = None
+            if e is not None:
+                self.graphs.move_to_end(key)
+                return g
         if any(m is not model for m, _ in self.graphs.values()):
             # another model (a re-loaded checkpoint or another precision plan): the model cache holds one
             # model, so drop its graphs -- they keep its handle (workspace, weights) alive
@@ -350,7 +353,7 @@ class _Staging:
         g = h.photo_graph(self.h_img, img3, self.x, self.m, native.MASK_U8, self.b, CROP_PAD, self.r, self.s,
                           target.view(self.hm.shape), self.hb, self.hr, self.hs)
         self.graphs[key] = (model, g)
-        while len(self.graphs) > self.MAX_GRAPHS * (1 if self.retarget else self.MASK_POOL + 1):
+        while len(self.graphs) > self.MAX_GRAPHS:
             self.graphs.popitem(last=False)[1][1].close()
         return g
 
@@ -380,7 +383,7 @@ def run_unet(pil_img: Image.Image, checkpoint_path: str, compute_dtype: str | No
             try:
                 g.launch(stream.cuda_stream)
             except RuntimeError:   # stale (the cached model's workspace grew, e.g. run_unet_batch): capture again
-                st.drop_graph(st.graph_key(img, target))
+                st.drop_graph(st.graph_key(img))
                 st.photo_graph(model, img, target).launch(stream.cuda_stream)
             stream.synchronize()
             # the kernel writes 0 / 1 bytes: bool views of the lent block, or a copy out of the shared buffer
