@@ -258,7 +258,8 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
   const int nch = L.cin / chunk;
   if (L.cin % chunk) return best;
   const int tw = cfg_tile_w(L.cfg), th = cfg_tile_h(L.cfg);
-  const int cap = ring8 ? 256 : 512;   // resident blocks: one 512-thread ring block / two halo blocks per CU
+  // resident blocks: one 512-thread ring block / two halo blocks per CU (the three-term 128-row tiles: one)
+  const int cap = (ring8 || (L.x3 == 2 && L.cfg == CFG_HALO_R128)) ? 256 : 512;
   // per-CU FLOP/s of the family and the partials' effective write + read rate, fitted to the batch-1
   // per-layer times with and without the split (profiles/tune_r4b_bs1_ksplit_*.txt: 134 MB of fp32
   // partials cost ~42 us = 3.2 TB/s including the reduction's launch)
@@ -776,7 +777,8 @@ std::string layer_label(const unet_handle* h, const Layer& L, int epi, Split sp 
                   cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0,
                   tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto), cfg_tile_h(cfg), cfg_tile_w(cfg));
   } else {
-    const int wpx = cfg == CFG_HALO_R64_W8 ? 8 : 4, tc = cfg == CFG_HALO_R128 ? 8 : 4,
+    const int wpx = (cfg == CFG_HALO_R64_W8 || (L.x3 == 2 && cfg == CFG_HALO_R128)) ? 8 : 4,
+              tc = cfg == CFG_HALO_R128 ? 8 : 4,
               ns = L.x3 == 2 ? 2 : cfg == CFG_HALO_R128 ? 2 : 3;
     std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, 1, %d, %d, %d, %d, %d, %d>", tname(L.dt), wpx, tc, ns,
                   L.taps == 9 ? 3 : 1, epi, L.x3);
@@ -962,8 +964,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     const bool pool = i == D1B || i == D2B || i == D3B || i == D4B;
     if (cfg_is_halo(c) && (L.dto != L.dt || (pool && L.dtq != L.dt))) c = L.cout == 64 || pool ? CFG_RING_R64_T3 : CFG_RING_R128;
     if (c == CFG_RING_R128 && pool) c = CFG_RING_R64_T3;   // pooled 128-row 4-wave tiles spill: same family, 64 rows
-    if (h->f32x3 && f32) {   // the three-term plan runs on the pre-split 64-row halo tiles only
-      c = CFG_HALO_R64_W4;
+    if (h->f32x3 && f32) {   // the three-term plan: pre-split 64-row tiles, or 128-row 8-wave tiles (no head)
+      c = (cfgs[i] == CFG_HALO_R128 && L.cout % 128 == 0 && i != C1B) ? CFG_HALO_R128 : CFG_HALO_R64_W4;
       L.x3 = 2;
     }
     L.cfg = c;
