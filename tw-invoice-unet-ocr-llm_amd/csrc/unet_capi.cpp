@@ -258,8 +258,7 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
   const int nch = L.cin / chunk;
   if (L.cin % chunk) return best;
   const int tw = cfg_tile_w(L.cfg), th = cfg_tile_h(L.cfg);
-  // resident blocks: one 512-thread ring block / two halo blocks per CU (the three-term 128-row tiles: one)
-  const int cap = (ring8 || (L.x3 == 2 && L.cfg == CFG_HALO_R128)) ? 256 : 512;
+  const int cap = ring8 ? 256 : 512;   // resident blocks: one 512-thread ring block / two halo blocks per CU
   // per-CU FLOP/s of the family and the partials' effective write + read rate, fitted to the batch-1
   // per-layer times with and without the split (profiles/tune_r4b_bs1_ksplit_*.txt: 134 MB of fp32
   // partials cost ~42 us = 3.2 TB/s including the reduction's launch)
@@ -274,7 +273,17 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
   const int own = cfg_rows(L.cfg);
   // the LDS-halo family's per-CU rate: exact-fp32 MFMA ~0.5 TF/s, the three-term plan ~0.85 TF/s (fp32 FLOPs)
   const double halo_rate = L.x3 ? 0.85e12 : 0.5e12;
-  double tbest = flops / ((double)std::min<long long>(tiles * (L.ctot / own), 256) * (ring8 ? 6e12 : halo_rate));
+  // CUs' worth of throughput from `blocks` resident blocks.  The three-term 64-row tiles run two blocks per CU,
+  // and a CU holding only one runs at ~0.6 of its two-block rate (the second block covers the first one's
+  // split and halo waits): count the first 256 blocks at 0.6 and the next 256 at 0.4 (fitted to the batch-1
+  // sweep of forced slice counts, gpurun_out/bs1_sweep_r6i_fp32.txt: every deep layer fastest at 512 blocks)
+  const bool two_tier = !ring8 && L.x3 == 2 && cap == 512;
+  auto cu_eq = [&](long long blocks) -> double {
+    if (!two_tier) return (double)std::min<long long>(blocks, 256);
+    return 0.6 * (double)std::min<long long>(blocks, 256) +
+           0.4 * (double)std::max<long long>(0, std::min<long long>(blocks, 512) - 256);
+  };
+  double tbest = flops / (cu_eq(tiles * (L.ctot / own)) * (ring8 ? 6e12 : halo_rate));
   for (int rows : {own, ring8 ? 64 : 0}) {
     if (rows == 0) break;
     const double rate = ring8 ? (rows == 128 ? 6e12 : 4.8e12) : halo_rate;
@@ -286,11 +295,11 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
       continue;
     }
     if (rows != own && epi != EPI_UPSCATTER) {   // finer row tiles alone, no K split (no partials)
-      const double t = flops / ((double)std::min<long long>(blocks, 256) * rate);
+      const double t = flops / (cu_eq(blocks) * rate);
       if (t < 0.9 * tbest) { tbest = t; best = {1, rows}; }
     }
     for (int ks = 2; ks <= h->ksplit_max && nch % ks == 0 && nch / ks >= (ring8 ? 2 : 1) && blocks * ks <= cap; ks *= 2) {
-      const double t = flops / ((double)std::min<long long>(blocks * ks, 256) * rate) + ks * P * L.ctot * 8.0 / bw + t_launch;
+      const double t = flops / (cu_eq(blocks * ks) * rate) + ks * P * L.ctot * 8.0 / bw + t_launch;
       if (t < 0.9 * tbest) { tbest = t; best = {ks, rows == own ? 0 : rows}; }   // a split must win by 10 %
     }
   }
@@ -777,8 +786,7 @@ std::string layer_label(const unet_handle* h, const Layer& L, int epi, Split sp 
                   cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0,
                   tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto), cfg_tile_h(cfg), cfg_tile_w(cfg));
   } else {
-    const int wpx = (cfg == CFG_HALO_R64_W8 || (L.x3 == 2 && cfg == CFG_HALO_R128)) ? 8 : 4,
-              tc = cfg == CFG_HALO_R128 ? 8 : 4,
+    const int wpx = cfg == CFG_HALO_R64_W8 ? 8 : 4, tc = cfg == CFG_HALO_R128 ? 8 : 4,
               ns = L.x3 == 2 ? 2 : cfg == CFG_HALO_R128 ? 2 : 3;
     std::snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%s, 1, %d, %d, %d, %d, %d, %d>", tname(L.dt), wpx, tc, ns,
                   L.taps == 9 ? 3 : 1, epi, L.x3);
@@ -964,8 +972,8 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     const bool pool = i == D1B || i == D2B || i == D3B || i == D4B;
     if (cfg_is_halo(c) && (L.dto != L.dt || (pool && L.dtq != L.dt))) c = L.cout == 64 || pool ? CFG_RING_R64_T3 : CFG_RING_R128;
     if (c == CFG_RING_R128 && pool) c = CFG_RING_R64_T3;   // pooled 128-row 4-wave tiles spill: same family, 64 rows
-    if (h->f32x3 && f32) {   // the three-term plan: pre-split 64-row tiles, or 128-row 8-wave tiles (no head)
-      c = (cfgs[i] == CFG_HALO_R128 && L.cout % 128 == 0 && i != C1B) ? CFG_HALO_R128 : CFG_HALO_R64_W4;
+    if (h->f32x3 && f32) {   // the three-term plan runs on the pre-split 64-row halo tiles only
+      c = CFG_HALO_R64_W4;
       L.x3 = 2;
     }
     L.cfg = c;

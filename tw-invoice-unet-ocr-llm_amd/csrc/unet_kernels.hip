@@ -748,14 +748,10 @@ struct HaloGeom {
   static constexpr int WSLOT = X3 == 2 ? 3 * BR * 64 : BR * 128;
   static constexpr int WI = X3 == 2 ? WSLOT / (1024 * NW) : BR / (8 * NW);   // weight DMA instructions per wave
   static constexpr int NI = (NPIX + 7) / 8;                    // halo DMA pieces (X3 = 2)
-  // HDB (X3 = 2 with 128-row tiles: 8 waves, one block per CU): two halo buffers, the next chunk's halo DMA'd
-  // two steps before the chunk ends; every wave issues HI pieces (the last ones land in slack rows)
-  static constexpr bool HDB = X3 == 2 && TC == 8;
-  static constexpr int HALO_BYTES = (X3 == 2 && !HDB) ? NI * 1024 : HI * NW * 8 * 128;
-  static constexpr int WOFF = HDB ? 2 * HALO_BYTES : HALO_BYTES;
+  static constexpr int HALO_BYTES = X3 == 2 ? NI * 1024 : HI * NW * 8 * 128;
+  static constexpr int WOFF = HALO_BYTES;
   static constexpr int PARAM_OFF = WOFF + NS * WSLOT;
   static constexpr int LDS_BYTES = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
-  static constexpr int BLOCKS_PER_CU = HDB ? 1 : 2;
 };
 
 // X3 (fp32 only): the fp32 operands as three bf16 terms (split3_bf16), 6 bf16 MFMAs per 32-K block instead of
@@ -764,16 +760,14 @@ struct HaloGeom {
 // three bf16 planes per step (no VALU for A, which the block's waves share), the activations are split on
 // the fly per fragment (the 3x3 layers).
 template <typename T, int WR, int WPX, int TCW, int NS, int KT, int EPI, int X3 = 0>
-__global__ __launch_bounds__(64 * WR * WPX, (X3 == 2 && TCW == 8) ? 2 : 2 * WR * WPX / 4)
-void conv3x3_halo_kernel(const IgemmArgs a) {
+__global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_kernel(const IgemmArgs a) {
   using G = HaloGeom<T, WR, WPX, TCW, NS, KT, X3>;
-  constexpr bool HDB = G::HDB;
   constexpr int NW = G::NW, TC = G::TC, TP = G::TP, BR = G::BR, BKE = G::BKE;
   constexpr int HWD = G::HWD, NPIX = G::NPIX, NTAP = G::NTAP, PAD = G::PAD;
   constexpr int HI = G::HI, WI = G::WI, WSLOT = G::WSLOT, WOFF = G::WOFF;
   static_assert(NS == 2 || NS == 3, "weight ring depth");
   static_assert(WI >= 1 && BR % (8 * NW) == 0, "weight tile split");
-  static_assert(G::LDS_BYTES <= 160 * 1024 / G::BLOCKS_PER_CU, "blocks per CU");
+  static_assert(G::LDS_BYTES <= 160 * 1024 / 2, "two blocks per CU");
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
   float* bias_s = reinterpret_cast<float*>(lds + G::PARAM_OFF);
   float* headw_s = bias_s + BR;
@@ -818,9 +812,9 @@ void conv3x3_halo_kernel(const IgemmArgs a) {
   const char* zero = reinterpret_cast<const char*>(a.zero);
   const long long pix0 = (long long)(n * H + ty * 16) * W + tx * 16;
 
-  auto issue_halo = [&](int c, int hb = 0) {
-    constexpr bool RR = X3 == 2 && !HDB;   // round-robin pieces, NI in all
-    char* dst = lds + hb * G::HALO_BYTES + wave * HI * 8 * 128;
+  auto issue_halo = [&](int c) {
+    constexpr bool RR = X3 == 2;   // round-robin pieces, NI in all
+    char* dst = lds + wave * HI * 8 * 128;
     const long long c0 = (long long)c * BKE;
 #pragma unroll
     for (int j = 0; j < HI; ++j) {
@@ -906,9 +900,9 @@ void conv3x3_halo_kernel(const IgemmArgs a) {
 
   // X3: the step's 32 K as one 16x16x32 block per fragment pair -- lane (col, q) holds K chunks q and
   // 4 + q (the kk = 0 and 1 fragments of read_frags), for A and B alike
-  auto x3_step = [&](int g, int tp, int hb) {
+  auto x3_step = [&](int g, int tp) {
     static_assert(X3 == 0 || sizeof(T) == 4, "X3 splits fp32 operands");
-    const char* hal = lds + hb * G::HALO_BYTES;   // this chunk's halo buffer (HDB: two)
+    const char* hal = lds;
     const int dy = tp / KT, dx = tp - (tp / KT) * KT;
     const char* Ws = lds + WOFF + (g % NS) * WSLOT + (wr * 16 * TC + col) * 128;
     const int toff = dy * HWD + dx;
@@ -1022,11 +1016,8 @@ void conv3x3_halo_kernel(const IgemmArgs a) {
   for (int g = 0; g < S; ++g) {
     const bool wnext = g + NS - 1 < S;
     if (wnext) issue_w(g + NS - 1);
-    if constexpr (HDB) {   // the next chunk's halo into the other buffer, after this step's weight DMA
-      if (tap == NTAP - 2 && c + 1 < nch) issue_halo(c_lo + c + 1, (c + 1) & 1);
-    }
     if constexpr (X3 != 0) {
-      x3_step(g, tap, HDB ? (c & 1) : 0);
+      x3_step(g, tap);
     } else {
       read_frags(g, tap, 0, a0, b0);
       mfmas(a0, b0);
@@ -1036,17 +1027,12 @@ void conv3x3_halo_kernel(const IgemmArgs a) {
       mfmas(a1, b1);
     }
     // the next step needs W(g+1); the barrier's lgkmcnt(0) also retires this step's reads (WAR)
-    if constexpr (HDB) {
-      static_assert(NS == 2, "HDB: two weight slots");
-      // the halo pieces issued this step (after W(g+1)) stay in flight through the wait for W(g+1); the last
-      // tap's wait then retires them: two steps of cover for the only operand that comes from HBM
-      if (tap == NTAP - 2 && c + 1 < nch) wait_vm_barrier<HI>(); else wait_vm_barrier<0>();
-    } else if (NS == 2) {
+    if (NS == 2) {
       wait_vm_barrier<0>();
     } else {
       if (wnext) wait_vm_barrier<WI>(); else wait_vm_barrier<0>();
     }
-    if (!HDB && tap == NTAP - 1 && c + 1 < nch) {   // every wave has finished reading the halo (barrier above)
+    if (tap == NTAP - 1 && c + 1 < nch) {   // every wave has finished reading the halo (barrier above)
 #ifdef UNET_ABL_X3_NOHALO   // timing-only ablation build: the chunk's halo is never reloaded
       if constexpr (X3 == 0)
 #endif
@@ -2668,14 +2654,6 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
       if (a.x3 == 2) {
         hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, 2, KT, EPI, 2>), dim3((unsigned)nb),
                            dim3(64 * WR * WPX), 0, s, a);
-        return hipGetLastError();
-      }
-    }
-    // 128-row tiles (CFG_HALO_R128): 8 waves of 128 rows x 32 pixels, one block per CU, two halo buffers --
-    // every activation split feeds 8 row groups (twice the 64-row tiles' MFMAs per split)
-    if constexpr (sizeof(T) == 4 && TCW == 8 && KT == 3 && EPI != EPI_HEAD) {
-      if (a.x3 == 2) {
-        hipLaunchKernelGGL((conv3x3_halo_kernel<T, 1, 8, 8, 2, KT, EPI, 2>), dim3((unsigned)nb), dim3(512), 0, s, a);
         return hipGetLastError();
       }
     }
