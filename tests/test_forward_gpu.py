@@ -1053,8 +1053,9 @@ def test_product_configs_build_no_spilling_kernels(monkeypatch):
     sd = syn.make_state_dict(int(z["seed"]), 3, 3, profile=str(z["profile"]))
     for cfg, dtype, want in ((8, "fp32_exact", "conv3x3_ring8_kernel<float, 4, 2,"),
                              (3, "bf16", "conv3x3_ring_kernel<__bf16, 1, 4, 4,"),
-                             # the three-term fp32 plan runs only on its pre-split 64-row halo tiles
-                             (8, "fp32", "conv3x3_halo_kernel<float, 1, 4, 4, ")):
+                             # the three-term fp32 plan runs only on its own tiles: split-once 128-row
+                             # tiles where Cout >= 128 (down2.3), the pre-split 64-row halo tiles elsewhere
+                             (8, "fp32", "conv3x3_x3s_kernel<1>")):
         monkeypatch.setenv("UNET_MI355X_CFG", ",".join(f"{i}:{cfg}" for i in range(17)))
         m = make_model(sd, 3, dtype)
         labels = m.native_handle(torch.device(DEV)).launch_labels()
@@ -1318,6 +1319,7 @@ def test_photo_graph_eviction_beside_batch_calls_on_another_thread():
         st = inf._staging[str(inf.DEVICE)]
         old_max = st.MAX_GRAPHS
         st.MAX_GRAPHS = 1
+        st.drop_graphs()    # (the LRU evicts on insertion: start from none, so every call below inserts)
         errors, stop = [], threading.Event()
 
         def batch_worker():

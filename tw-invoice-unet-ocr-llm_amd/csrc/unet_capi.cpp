@@ -137,7 +137,8 @@ struct unet_handle {
   // (UNET_MI355X_KSPLIT_FORCE="i:ks,...", i = 3x3 layer 0..16 or 17 + ConvTranspose 0..3; 0 = auto;
   // ks + 100 = ks slices on 64-row tiles of the 8-wave ring)
   int ksplit_max = 32;
-  int f32x3 = 0;   // fp32 plan: 1 = operands as three bf16 terms on the bf16 MFMA pipe (IgemmArgs::x3)
+  int f32x3 = 0;   // fp32 plan: operands as three bf16 terms on the bf16 MFMA pipe (IgemmArgs::x3): 2 = split-once
+                   // 128-row tiles on the Cout >= 128 layers, 1 = 64-row tiles everywhere
   int ksplit_force[21] = {};
   void* part = nullptr;   // the current forward's partial buffer (workspace region Buffers::part)
   // mask-box sync entries (launch_mask_boxes: kSyncInts ints per (image, field), idle between
@@ -258,7 +259,8 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
   const int nch = L.cin / chunk;
   if (L.cin % chunk) return best;
   const int tw = cfg_tile_w(L.cfg), th = cfg_tile_h(L.cfg);
-  const int cap = ring8 ? 256 : 512;   // resident blocks: one 512-thread ring block / two halo blocks per CU
+  // resident blocks: one 512-thread block per CU (the 8-wave ring, the split-once three-term tiles) / two halo blocks
+  const int cap = ring8 || L.x3 == 3 ? 256 : 512;
   // per-CU FLOP/s of the family and the partials' effective write + read rate, fitted to the batch-1
   // per-layer times with and without the split (profiles/tune_r4b_bs1_ksplit_*.txt: 134 MB of fp32
   // partials cost ~42 us = 3.2 TB/s including the reduction's launch)
@@ -271,8 +273,9 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
   // candidate row tiles: the layer's own; on the ring also 64-row halves (twice the blocks per slice, so
   // half the slices for the same CU count; 0.8x the per-CU rate: half the MFMAs per halo byte)
   const int own = cfg_rows(L.cfg);
-  // the LDS-halo family's per-CU rate: exact-fp32 MFMA ~0.5 TF/s, the three-term plan ~0.85 TF/s (fp32 FLOPs)
-  const double halo_rate = L.x3 ? 0.85e12 : 0.5e12;
+  // the LDS-halo family's per-CU rate: exact-fp32 MFMA ~0.5 TF/s, the three-term plan ~0.85 TF/s (fp32 FLOPs) on
+  // 64-row tiles, ~1.1 on the split-once 128-row tiles (a first estimate: to be fitted on the batch-1 sweep)
+  const double halo_rate = L.x3 == 3 ? 1.1e12 : L.x3 ? 0.85e12 : 0.5e12;
   // CUs' worth of throughput from `blocks` resident blocks.  The three-term 64-row tiles run two blocks per CU,
   // and a CU holding only one runs at ~0.6 of its two-block rate (the second block covers the first one's
   // split and halo waits): count the first 256 blocks at 0.6 and the next 256 at 0.4 (fitted to the batch-1
@@ -499,7 +502,7 @@ int pack3x3_split(const Layer& L, const std::vector<double>& w, std::vector<uint
 }
 
 int pack3x3_host(const Layer& L, const std::vector<double>& w, std::vector<uint8_t>& buf) {
-  if (L.x3 == 2) return pack3x3_split(L, w, buf);
+  if (L.x3 == 2 || L.x3 == 3) return pack3x3_split(L, w, buf);
   const int K = 9 * L.cin;
   buf.assign((size_t)L.cout * K * dtype_size(L.dt), 0);
   const bool ring = cfg_is_ring(L.cfg);
@@ -785,6 +788,8 @@ std::string layer_label(const unet_handle* h, const Layer& L, int epi, Split sp 
     std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %s, %s, %d, %d>", tname(L.dt),
                   cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0,
                   tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto), cfg_tile_h(cfg), cfg_tile_w(cfg));
+  } else if (L.x3 == 3) {
+    std::snprintf(buf, sizeof buf, "conv3x3_x3s_kernel<%d>", epi);
   } else {
     const int wpx = cfg == CFG_HALO_R64_W8 ? 8 : 4, tc = cfg == CFG_HALO_R128 ? 8 : 4,
               ns = L.x3 == 2 ? 2 : cfg == CFG_HALO_R128 ? 2 : 3;
@@ -935,8 +940,10 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
   unet_handle* h = new unet_handle();
   h->cfg = *cfg;
   const bool f32 = cfg->dtype == UNET_DTYPE_F32 || cfg->dtype == UNET_DTYPE_F32_EXACT;
-  h->f32x3 = cfg->dtype == UNET_DTYPE_F32;
-  if (const char* x3 = std::getenv("UNET_MI355X_F32X3")) h->f32x3 = f32 && std::atoi(x3) != 0;   // A/B runs
+  // the three-term plan: 2 = the split-once 128-row tiles on the Cout >= 128 layers (x3 = 3), 64-row tiles
+  // splitting per tap elsewhere (x3 = 2); 1 = x3 = 2 everywhere; 0 = exact fp32 (UNET_MI355X_F32X3: A/B runs)
+  h->f32x3 = cfg->dtype == UNET_DTYPE_F32 ? 2 : 0;
+  if (const char* x3 = std::getenv("UNET_MI355X_F32X3")) h->f32x3 = f32 ? std::atoi(x3) : 0;
   h->dt = f32 ? DType::F32 : DType::BF16;   // workspace element size (all 16-bit plans: 2 bytes)
   for (int i = 0; i < kMaxClasses; ++i) h->thr_logit[i] = unet_logit_cut(cfg->thresholds[i]);
   // Kernel configuration per layer (tuned on MI355X).  A/B override for tuning:
@@ -972,9 +979,10 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     const bool pool = i == D1B || i == D2B || i == D3B || i == D4B;
     if (cfg_is_halo(c) && (L.dto != L.dt || (pool && L.dtq != L.dt))) c = L.cout == 64 || pool ? CFG_RING_R64_T3 : CFG_RING_R128;
     if (c == CFG_RING_R128 && pool) c = CFG_RING_R64_T3;   // pooled 128-row 4-wave tiles spill: same family, 64 rows
-    if (h->f32x3 && f32) {   // the three-term plan runs on the pre-split 64-row halo tiles only
-      c = CFG_HALO_R64_W4;
-      L.x3 = 2;
+    if (h->f32x3 && f32) {   // the three-term plan: pre-split weights on 128-row split-once or 64-row tiles
+      const bool once = h->f32x3 == 2 && L.cout % 128 == 0 && i != C1B;
+      c = once ? CFG_HALO_R128 : CFG_HALO_R64_W4;
+      L.x3 = once ? 3 : 2;
     }
     L.cfg = c;
   }

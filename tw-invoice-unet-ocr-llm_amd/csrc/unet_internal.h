@@ -66,7 +66,9 @@ struct IgemmArgs {
   int src_br;   // EPI_PARTIAL on the 8-wave ring: row tile of the weight packing when finer than BR (0 = BR)
   int x3;       // fp32 LDS-halo family: 0 = exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); fp32 operands as three
                 // bf16 terms (6 bf16 MFMAs per 32 K): 1 = both split on the fly (the ConvTranspose), 2 = weights
-                // pre-split by the packing, activations on the fly (3x3 layers, CFG_HALO_R64_W4)
+                // pre-split by the packing, activations on the fly (3x3 layers, CFG_HALO_R64_W4), 3 = weights
+                // pre-split, activations split once per chunk into LDS planes (conv3x3_x3s_kernel,
+                // CFG_HALO_R128: the 3x3 layers with Cout >= 128)
 };
 
 struct FirstConvArgs {

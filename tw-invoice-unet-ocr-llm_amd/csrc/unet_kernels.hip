@@ -126,6 +126,11 @@ __device__ __forceinline__ f32x4 mfma16<float>(const uint2&, const uint2&, const
 // |a b|: fp32 accuracy (unet_model.py:10,14 in fp32) at 6 MFMAs of 16x16x32 (6 x 16 cycles) where the
 // exact-fp32 path needs 8 of 16x16x4 f32 (8 x 32 cycles) for the same 32 K.  x0, x1: the 8 fp32 K values of
 // this lane (two 16-byte fragments); A and B are split with the same K order.
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE), lo in bits 0..15
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
+}
 __device__ __forceinline__ void split3_bf16(const frag_t& x0, const frag_t& x1, frag_t& h, frag_t& m, frag_t& l) {
 #ifdef UNET_ABL_X3_NOSPLIT   // timing-only ablation build: no split arithmetic (operand bits reused as terms)
   h = x0;
@@ -133,21 +138,20 @@ __device__ __forceinline__ void split3_bf16(const frag_t& x0, const frag_t& x1, 
   l = x0;
   return;
 #endif
+  // per pair of values: one v_cvt_pk_bf16_f32 per term and the two halves widened back with a shift / a
+  // mask (11 VALU per pair; the element-wise form compiled to ~14 with single-value conversions)
   const f32x4 a = __builtin_bit_cast(f32x4, x0), b = __builtin_bit_cast(f32x4, x1);
-  bf16x8 H, M, L;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const float v = i < 4 ? a[i] : b[i - 4];
-    const __bf16 hi = (__bf16)v;
-    const float r = v - (float)hi;
-    const __bf16 mi = (__bf16)r;
-    H[i] = hi;
-    M[i] = mi;
-    L[i] = (__bf16)(r - (float)mi);
+  for (int i = 0; i < 4; ++i) {
+    const float v0 = i < 2 ? a[2 * i] : b[2 * i - 4], v1 = i < 2 ? a[2 * i + 1] : b[2 * i - 3];
+    const uint32_t hp = cvt_pk_bf16(v0, v1);
+    const float r0 = v0 - __uint_as_float(hp << 16), r1 = v1 - __uint_as_float(hp & 0xffff0000u);
+    const uint32_t mp = cvt_pk_bf16(r0, r1);
+    const float s0 = r0 - __uint_as_float(mp << 16), s1 = r1 - __uint_as_float(mp & 0xffff0000u);
+    h[i] = (int)hp;
+    m[i] = (int)mp;
+    l[i] = (int)cvt_pk_bf16(s0, s1);
   }
-  h = __builtin_bit_cast(frag_t, H);
-  m = __builtin_bit_cast(frag_t, M);
-  l = __builtin_bit_cast(frag_t, L);
 }
 __device__ __forceinline__ void mfma_bf16(f32x4& acc, const frag_t& a, const frag_t& b) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
@@ -1053,6 +1057,190 @@ __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_
                                    wp * TP, ct * BR + wr * 16 * TC + 64 * h, bias_s + wr * 16 * TC + 64 * h, headw_s,
                                    headb_s);
   }
+}
+
+// ---------------------------------------------------------------------------------
+// three-term fp32 with the activations split once per chunk (IgemmArgs::x3 = 3)
+// ---------------------------------------------------------------------------------
+// The X3 = 2 halo kernel above splits an activation fragment at every tap that reads it (nine splits of
+// each halo value per row tile): ~176 VALU per wave and K step beside its 96 MFMAs, and a 16x16x32 MFMA
+// leaves the SIMD's vector issue free for only 8 of its 16 cycles (MI355X_MICROARCH.md, constants table),
+// so that step is vector-issue bound.  Here the block splits each 32-channel chunk's halo ONCE, into three
+// bf16 planes in LDS, from an fp32 staging copy the LDS DMA filled during the previous chunk; the nine
+// taps then read the planes (per wave and step: 96 MFMAs, 24 ds_read_b128, no conversion).  Staging
+// (41 KB) + planes (62 KB) + two 24 KB weight slots take 151 KB: one 8-wave block per CU, 128 rows x
+// 16x16 pixels (a 64-row x 64-pixel tile per wave, two waves per SIMD), for the layers with Cout >= 128.
+// The same products in the same order per accumulator as X3 = 2 (bitwise the same sums per K slice).
+// Planes: halo pixel r = hy * 18 + hx is a 64-byte row per plane; its 16-byte piece q (K values 4q..4q+3,
+// 16+4q..16+4q+3, the weight planes' order) sits at q ^ ((hy & 1) << 1), so each ds_read_b128 lane group
+// (4 pixels of row y and 4 of row y + 1, two pieces) covers the 64 banks once at every tap
+// (tests/test_lds_layout_cpu.py).
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void conv3x3_x3s_kernel(const IgemmArgs a) {
+  constexpr int NW = 8, WPX = 4, TC = 4, TP = 4, BR = 128, HWD = 18, NPIX = HWD * HWD, NTAP = 9;
+  constexpr int NI = (NPIX + 7) / 8;        // staging DMA pieces (8 halo pixels x 128 B)
+  constexpr int HJ = (NI + NW - 1) / NW;    // per wave (the last round's surplus repeats piece NI - 1)
+  constexpr int PLANE = NPIX * 64;
+  constexpr int SPL = NI * 1024;            // the planes follow the staging buffer
+  constexpr int WSLOT = 3 * BR * 64;
+  constexpr int WJ = WSLOT / (1024 * NW);   // weight DMA pieces per wave and step
+  constexpr int WOFF = SPL + 3 * PLANE;
+  constexpr int PARAM_OFF = WOFF + 2 * WSLOT;
+  constexpr int LDS_BYTES = PARAM_OFF + BR * 4;
+  static_assert(LDS_BYTES <= 160 * 1024 && WSLOT % (1024 * NW) == 0, "one 8-wave block per CU");
+  static_assert(SPL % 256 == 0 && PLANE % 256 == 0 && WOFF % 256 == 0, "bank-aligned regions");
+  static_assert(EPI == EPI_STORE || EPI == EPI_POOL || EPI == EPI_PARTIAL, "x3s epilogues");
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  float* bias_s = reinterpret_cast<float*>(lds + PARAM_OFF);
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wr = wave / WPX;
+  const int wp = wave % WPX;
+  int bid;
+  {  // XCD-contiguous remap (as conv3x3_halo_kernel)
+    const int nb = gridDim.x, qq = nb >> 3, rr = nb & 7;
+    const int b = blockIdx.x, x = b & 7, k = b >> 3;
+    bid = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + k;
+  }
+  constexpr bool PART = EPI == EPI_PARTIAL;
+  const int KS = PART ? a.ksplit : 1;
+  const int ct = bid % a.n_ct;
+  int mt = bid / a.n_ct;
+  const int kslice = PART ? mt % KS : 0;
+  if (PART) mt /= KS;
+  const int tx = mt % a.tiles_x;
+  mt /= a.tiles_x;
+  const int ty = mt % a.tiles_y;
+  const int n = mt / a.tiles_y;
+  if (n >= a.N) return;
+
+  const int H = a.H, W = a.W;
+  const int nch = a.Cin / 32 / KS;
+  const int c_lo = kslice * nch;
+  const int S = NTAP * nch;
+  const char* in = reinterpret_cast<const char*>(a.in);
+  const char* zero = reinterpret_cast<const char*>(a.zero);
+  const long long pix0 = (long long)(n * H + ty * 16) * W + tx * 16;
+
+  auto issue_halo = [&](int c) {   // chunk c's fp32 halo -> staging row r at r * 128, piece k at k ^ (hx & 7)
+    const long long c0 = (long long)c * 32;
+#pragma unroll
+    for (int j = 0; j < HJ; ++j) {
+      const int piece = min(j * NW + wave, NI - 1);
+      const int row = piece * 8 + (lane >> 3);
+      const int hy = row / HWD, hx = row - hy * HWD;
+      const int iy = ty * 16 + hy - 1, ix = tx * 16 + hx - 1;
+      const bool ok = row < NPIX && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const int chk = ((lane & 7) ^ (hx & 7)) * 16;
+      const long long pix = pix0 + (long long)(hy - 1) * W + (hx - 1);
+      const char* src = ok ? in + (pix * a.ldi + c0) * 4LL + chk : zero + chk;
+      glds16(src, lds + piece * 1024);
+    }
+  };
+  auto issue_w = [&](int g) {   // step g's pre-split weights [3][BR][64 B] (unet_capi.cpp pack3x3_split)
+    const long long step = (long long)ct * (NTAP * (a.Cin / 32)) + (long long)c_lo * NTAP + g;
+    const char* src = reinterpret_cast<const char*>(a.wgt) + step * WSLOT + (wave * WJ) * 1024 + lane * 16;
+    char* dst = lds + WOFF + (g & 1) * WSLOT + wave * WJ * 1024;
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) glds16(src + j * 1024, dst + j * 1024);
+  };
+  auto split_halo = [&]() {   // staging -> planes, one (pixel, piece) per thread and round
+#pragma unroll
+    for (int k = 0; k < (NPIX * 4 + 64 * NW - 1) / (64 * NW); ++k) {
+      const int u = tid + k * 64 * NW;
+      if (u < NPIX * 4) {
+        const int r = u >> 2, pq = u & 3;
+        const int hy = r / HWD, hx7 = (r - hy * HWD) & 7;
+        const char* sp = lds + r * 128;
+        const frag_t x0 = *reinterpret_cast<const frag_t*>(sp + ((pq ^ hx7) << 4));
+        const frag_t x1 = *reinterpret_cast<const frag_t*>(sp + (((4 + pq) ^ hx7) << 4));
+        frag_t h, m, l;
+        split3_bf16(x0, x1, h, m, l);
+        char* dp = lds + SPL + r * 64 + ((pq ^ ((hy & 1) << 1)) << 4);
+        *reinterpret_cast<frag_t*>(dp) = h;
+        *reinterpret_cast<frag_t*>(dp + PLANE) = m;
+        *reinterpret_cast<frag_t*>(dp + 2 * PLANE) = l;
+      }
+    }
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int t = 0; t < TC; ++t)
+#pragma unroll
+    for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int col = lane & 15, q = lane >> 4;
+  int prow[TP];
+#pragma unroll
+  for (int p = 0; p < TP; ++p) {
+    int py, px;
+    pix_of((wp * TP + p) * 16 + col, py, px);
+    prow[p] = py * HWD + px;
+  }
+  const int ylo = (col >> 3) & 1;   // hy & 1 of this lane's pixels at dy = 0 (pix_of: row pairs)
+  const char* Wl = lds + WOFF + (wr * 16 * TC + col) * 64 + ((q ^ ((col >> 1) & 3)) << 4);
+
+  issue_halo(c_lo);
+  issue_w(0);
+  for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];
+  wait_vm_barrier<0>();
+  split_halo();
+  wait_vm_barrier<0>();
+
+  int c = 0, tap = 0;
+  for (int g = 0; g < S; ++g) {
+    if (g + 1 < S) issue_w(g + 1);
+    // the next chunk's halo into the (free) staging buffer, behind W(g + 1): in flight for two steps
+    const bool hnext = tap == 0 && c + 1 < nch;
+    if (hnext) issue_halo(c_lo + c + 1);
+    {
+      const int dy = tap / 3, dx = tap - dy * 3;
+      const char* Wp = Wl + (g & 1) * WSLOT;
+      frag_t ah[TC], am[TC], al[TC];
+#pragma unroll
+      for (int t = 0; t < TC; ++t) {
+        ah[t] = *reinterpret_cast<const frag_t*>(Wp + t * 16 * 64);
+        am[t] = *reinterpret_cast<const frag_t*>(Wp + BR * 64 + t * 16 * 64);
+        al[t] = *reinterpret_cast<const frag_t*>(Wp + 2 * BR * 64 + t * 16 * 64);
+      }
+      const char* Bl = lds + SPL + (dy * HWD + dx) * 64 + ((q ^ (((ylo ^ dy) & 1) << 1)) << 4);
+#pragma unroll
+      for (int p = 0; p < TP; ++p) {
+        const char* bp = Bl + prow[p] * 64;
+        const frag_t bh = *reinterpret_cast<const frag_t*>(bp);
+        const frag_t bm = *reinterpret_cast<const frag_t*>(bp + PLANE);
+        const frag_t bl = *reinterpret_cast<const frag_t*>(bp + 2 * PLANE);
+        // the X3 = 2 order per accumulator: small terms first
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], am[t], bm);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], al[t], bh);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], ah[t], bl);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], am[t], bh);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], ah[t], bm);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], ah[t], bh);
+      }
+    }
+    // W(g + 1) landed (and the halo, one step later); the barrier's lgkmcnt(0) retires this step's reads
+    if (hnext) wait_vm_barrier<HJ>(); else wait_vm_barrier<0>();
+    if (tap == NTAP - 1 && c + 1 < nch) {   // every wave is past the chunk's last tap: refill the planes
+      split_halo();
+      wait_vm_barrier<0>();
+    }
+    if (++tap == NTAP) { tap = 0; ++c; }
+  }
+  const int row0 = ct * BR + wr * 16 * TC;
+  if constexpr (PART)
+    partial_store<TP, 16>(a, acc, n, ty * 16, tx * 16, wp * TP, row0, kslice);
+  else
+    conv_epilogue<float, float, TP, EPI>(a, acc, n, ty * 16, tx * 16, wp * TP, row0, bias_s + wr * 16 * TC, nullptr,
+                                         nullptr);
 }
 
 
@@ -2650,6 +2838,13 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
                 // pre-split weights (two weight slots: a third beside the exactly sized halo fits, 78 KB, but
                 // measured 2 % slower), the
                 // ConvTranspose with both operands split on the fly
+    if constexpr (sizeof(T) == 4 && WPX == 4 && TCW == 8 && KT == 3 &&
+                  (EPI == EPI_STORE || EPI == EPI_POOL || EPI == EPI_PARTIAL)) {
+      if (a.x3 == 3) {   // 128-row tiles, the activations split once per chunk (conv3x3_x3s_kernel)
+        hipLaunchKernelGGL((conv3x3_x3s_kernel<EPI>), dim3((unsigned)nb), dim3(512), 0, s, a);
+        return hipGetLastError();
+      }
+    }
     if constexpr (sizeof(T) == 4 && WPX == 4 && TCW == 4 && KT == 3) {
       if (a.x3 == 2) {
         hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, 2, KT, EPI, 2>), dim3((unsigned)nb),
