@@ -61,39 +61,44 @@ def test_presplit_weight_reads_are_conflict_free():
             assert sorted(banks) == list(range(64)), (t, g)
 
 
-def _pix_of(p):
-    """unet_kernels.hip pix_of: pixel p of a 16x16 tile -> (row, col), groups of 2 rows x 8 columns."""
+def _pix_of(p, tw=16):
+    """unet_kernels.hip pix_of_w<TW>: pixel p of a 16 x TW tile -> (row, col), groups of 2 rows x 8 columns."""
     g, j = p >> 4, p & 15
-    return 2 * (g >> 1) + (j >> 3), 8 * (g & 1) + (j & 7)
+    return 2 * (g // (tw // 8)) + (j >> 3), 8 * (g % (tw // 8)) + (j & 7)
 
 
 def test_split_once_plane_reads_are_conflict_free_at_every_tap():
-    """The split-once three-term kernel (conv3x3_x3s_kernel): each activation plane holds halo pixel
-    r = hy * 18 + hx as a 64-byte row, piece q at q ^ ((hy & 1) << 1).  At every tap (dy, dx), for every
-    wave (wp) and pixel group, each ds_read_b128 lane group covers the 64 banks once; the kernel's
-    per-lane swizzle ((col >> 3) ^ dy) & 1 equals (hy & 1) of the pixel it reads."""
-    for wp in range(4):
-        for p in range(4):
-            for dy in range(3):
-                for dx in range(3):
-                    for g in B128_GROUPS:
-                        banks = []
-                        for lane in g:
-                            col, q = lane & 15, lane >> 4
-                            py, px = _pix_of((wp * 4 + p) * 16 + col)
-                            hy, hx = py + dy, px + dx
-                            assert (hy & 1) == (((col >> 3) ^ dy) & 1)
-                            addr = (hy * 18 + hx) * 64 + ((q ^ ((hy & 1) << 1)) << 4)
-                            banks += [(addr // 4 + i) % 64 for i in range(4)]
-                        assert sorted(banks) == list(range(64)), (wp, p, dy, dx, g)
+    """The split-once three-term kernels: each activation plane holds halo pixel r = hy * HWX + hx as a
+    64-byte row, piece q at q ^ ((hy & 1) << 1) -- conv3x3_x3s_kernel (16x16 tiles, HWX = 18, four waves of
+    four pixel groups per row group) and conv3x3_x3w_kernel (16x32 tiles, HWX = 34, eight waves).  At every
+    tap (dy, dx), for every wave and pixel group, each ds_read_b128 lane group covers the 64 banks once;
+    the kernels' per-lane swizzle ((col >> 3) ^ dy) & 1 equals (hy & 1) of the pixel read."""
+    for tw, waves in ((16, 4), (32, 8)):
+        hwx = tw + 2
+        for wp in range(waves):
+            for p in range(4):
+                for dy in range(3):
+                    for dx in range(3):
+                        for g in B128_GROUPS:
+                            banks = []
+                            for lane in g:
+                                col, q = lane & 15, lane >> 4
+                                py, px = _pix_of((wp * 4 + p) * 16 + col, tw)
+                                hy, hx = py + dy, px + dx
+                                assert (hy & 1) == (((col >> 3) ^ dy) & 1)
+                                addr = (hy * hwx + hx) * 64 + ((q ^ ((hy & 1) << 1)) << 4)
+                                banks += [(addr // 4 + i) % 64 for i in range(4)]
+                            assert sorted(banks) == list(range(64)), (tw, wp, p, dy, dx, g)
 
 
 def test_split_once_pass_covers_every_plane_piece_once():
-    """The split pass: unit u = (pixel u >> 2, piece u & 3) over 324 x 4 units writes each 16-byte piece of
-    each plane exactly once (a permutation of the pieces within every row)."""
-    seen = set()
-    for u in range(324 * 4):
-        r, pq = u >> 2, u & 3
-        hy = r // 18
-        seen.add(r * 64 + ((pq ^ ((hy & 1) << 1)) << 4))
-    assert seen == {r * 64 + 16 * k for r in range(324) for k in range(4)}
+    """The split pass: unit u = (pixel u >> 2, piece u & 3) over the halo's pixels x 4 units writes each
+    16-byte piece of each plane exactly once (a permutation of the pieces within every row)."""
+    for hwx in (18, 34):
+        npix = 18 * hwx
+        seen = set()
+        for u in range(npix * 4):
+            r, pq = u >> 2, u & 3
+            hy = r // hwx
+            seen.add(r * 64 + ((pq ^ ((hy & 1) << 1)) << 4))
+        assert seen == {r * 64 + 16 * k for r in range(npix) for k in range(4)}

@@ -105,6 +105,10 @@ struct unet_handle {
   float* b0 = nullptr;
   Layer L[17];          // d1b d2a d2b d3a d3b d4a d4b bna bnb c4a c4b c3a c3b c2a c2b c1a c1b
   Layer U[4];           // up4 up3 up2 up1
+  // the three-term plan's small-batch ConvTranspose (N <= kSmallBatch with the split-K plan on; w == nullptr
+  // otherwise): pre-split weights on 64-row tiles, where the large-batch plan's 128-row tiles split both
+  // operands on the fly -- the same products in the same order per accumulator (unsplit: bitwise the same)
+  Layer Us[4];
   // up1 fused into conv2.3 (EPI_UPFUSE, 16-bit plans): conv2.3's ring weights followed by 8
   // ConvTranspose steps (pack_fused_up); the forward then has no up1 launch and conv2.3's output
   // is never stored (unet_debug_fetch "c7" is unavailable).  UNET_MI355X_FUSE_UP1=0 disables it.
@@ -236,6 +240,10 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // LDS-halo family (fp32 plan, 3x3 and ConvTranspose) with a plain store, pool or scatter epilogue;
 // never the fused first conv, the head or the fused up1.
 constexpr int kSmallBatch = 4;
+// ConvTranspose j's layer at batch N: the small-batch variant Us[j] where the plan has one
+const Layer& up_layer(const unet_handle* h, int j, int N) {
+  return (h->Us[j].w && h->ksplit_max > 1 && N >= 1 && N <= kSmallBatch) ? h->Us[j] : h->U[j];
+}
 struct Split {
   int ks = 1;     // K slices (1 = the layer runs unsplit)
   int rows = 0;   // 8-wave ring: row tile of the slices (64 = halves of the 128-row packing), 0 = the layer's own
@@ -260,7 +268,7 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
   if (L.cin % chunk) return best;
   const int tw = cfg_tile_w(L.cfg), th = cfg_tile_h(L.cfg);
   // resident blocks: one 512-thread block per CU (the 8-wave ring, the split-once three-term tiles) / two halo blocks
-  const int cap = ring8 || L.x3 == 3 ? 256 : 512;
+  const int cap = ring8 || L.x3 >= 3 ? 256 : 512;
   // per-CU FLOP/s of the family and the partials' effective write + read rate, fitted to the batch-1
   // per-layer times with and without the split (profiles/tune_r4b_bs1_ksplit_*.txt: 134 MB of fp32
   // partials cost ~42 us = 3.2 TB/s including the reduction's launch)
@@ -275,7 +283,7 @@ Split layer_split(const unet_handle* h, int id, const Layer& L, int epi, int N, 
   const int own = cfg_rows(L.cfg);
   // the LDS-halo family's per-CU rate: exact-fp32 MFMA ~0.5 TF/s, the three-term plan ~0.85 TF/s (fp32 FLOPs) on
   // 64-row tiles, ~1.1 on the split-once 128-row tiles (a first estimate: to be fitted on the batch-1 sweep)
-  const double halo_rate = L.x3 == 3 ? 1.1e12 : L.x3 ? 0.85e12 : 0.5e12;
+  const double halo_rate = L.x3 >= 3 ? 1.1e12 : L.x3 ? 0.85e12 : 0.5e12;
   // CUs' worth of throughput from `blocks` resident blocks.  The three-term 64-row tiles run two blocks per CU,
   // and a CU holding only one runs at ~0.6 of its two-block rate (the second block covers the first one's
   // split and halo waits): count the first 256 blocks at 0.6 and the next 256 at 0.4 (fitted to the batch-1
@@ -326,7 +334,7 @@ size_t split_bytes(const unet_handle* h, int N, int H, int W) {
     one(i, h->L[i], epi, kLayerLevel[i]);
   }
   for (int j = 0; j < 4; ++j)
-    if (!(j == 3 && h->fuse_up1)) one(17 + j, h->U[j], EPI_UPSCATTER, kUpLevel[j]);
+    if (!(j == 3 && h->fuse_up1)) one(17 + j, up_layer(h, j, N), EPI_UPSCATTER, kUpLevel[j]);
   return m;
 }
 
@@ -479,6 +487,19 @@ void split3_host(float v, uint16_t (&t)[3]) {
 // step g = (32-channel chunk, tap) -- the halo kernel's step order -- three bf16 planes (hi, mid, lo) of
 // 64 rows x 64 B; in row r, 16-byte chunk q holds channels 4q..4q+3 and 16+4q..16+4q+3 of the chunk (the
 // K values lane group q of the activation fragments holds) at position q ^ ((r >> 1) & 3).
+// One row of a pre-split step block (blk = the block's byte offset, r = row in the tile): value(c) for the
+// chunk's 32 channels c = 32 * ch + ...
+template <typename F>
+void put_split_row(std::vector<uint8_t>& buf, size_t blk, int BR, int r, int ch, F value) {
+  for (int j = 0; j < 32; ++j) {   // bf16 slot j of the row: chunk q = j / 8, element e = j % 8
+    const int q = j >> 3, e = j & 7;
+    const int c = 32 * ch + (e < 4 ? 4 * q + e : 16 + 4 * q + e - 4);
+    uint16_t t[3];
+    split3_host((float)value(c), t);
+    const size_t off = (size_t)r * 64 + (size_t)((q ^ ((r >> 1) & 3)) * 16) + (size_t)e * 2;
+    for (int p = 0; p < 3; ++p) std::memcpy(&buf[blk + (size_t)p * BR * 64 + off], &t[p], 2);
+  }
+}
 int pack3x3_split(const Layer& L, const std::vector<double>& w, std::vector<uint8_t>& buf) {
   const int BR = cfg_rows(L.cfg), NCH = L.cin / 32, S = 9 * NCH;
   if (L.cout % BR || L.cin % 32) return fail(UNET_EINVAL, "pre-split weight tiling does not divide the layer");
@@ -486,23 +507,15 @@ int pack3x3_split(const Layer& L, const std::vector<double>& w, std::vector<uint
   for (int rho = 0; rho < L.cout; ++rho) {
     const int o = natural_of_packed(rho), ct = rho / BR, r = rho % BR;
     for (int ch = 0; ch < NCH; ++ch)
-      for (int tap = 0; tap < 9; ++tap) {
-        const size_t blk = ((size_t)ct * S + (size_t)ch * 9 + tap) * 3 * BR * 64;
-        for (int j = 0; j < 32; ++j) {   // bf16 slot j of the row: chunk q = j / 8, element e = j % 8
-          const int q = j >> 3, e = j & 7;
-          const int c = 32 * ch + (e < 4 ? 4 * q + e : 16 + 4 * q + e - 4);
-          uint16_t t[3];
-          split3_host((float)w[((size_t)o * L.cin + c) * 9 + tap], t);
-          const size_t off = (size_t)r * 64 + (size_t)((q ^ ((r >> 1) & 3)) * 16) + (size_t)e * 2;
-          for (int p = 0; p < 3; ++p) std::memcpy(&buf[blk + (size_t)p * BR * 64 + off], &t[p], 2);
-        }
-      }
+      for (int tap = 0; tap < 9; ++tap)
+        put_split_row(buf, ((size_t)ct * S + (size_t)ch * 9 + tap) * 3 * BR * 64, BR, r, ch,
+                      [&](int c) { return w[((size_t)o * L.cin + c) * 9 + tap]; });
   }
   return UNET_OK;
 }
 
 int pack3x3_host(const Layer& L, const std::vector<double>& w, std::vector<uint8_t>& buf) {
-  if (L.x3 == 2 || L.x3 == 3) return pack3x3_split(L, w, buf);
+  if (L.x3 >= 2) return pack3x3_split(L, w, buf);
   const int K = 9 * L.cin;
   buf.assign((size_t)L.cout * K * dtype_size(L.dt), 0);
   const bool ring = cfg_is_ring(L.cfg);
@@ -567,17 +580,28 @@ int pack_fused_up(unet_handle* h, const Layer& L, const Layer& U, const std::vec
 // ring kernel (cfg_is_tring) takes them in step order per BR-row tile: [ct][c / BKE][BR][BKE].
 int packT(unet_handle* h, Layer& L, const float* W, const float* B) {
   const int R = 4 * L.cout;
-  std::vector<uint8_t> buf((size_t)R * L.cin * dtype_size(L.dt));
-  const bool ring = cfg_is_tring(L.cfg);
-  const int BR = cfg_rows(L.cfg), BKE = 64 / (int)dtype_size(L.dt), S = L.cin / BKE;
-  if (ring && (R % BR || L.cin % BKE)) return fail(UNET_EINVAL, "ring ConvTranspose tiling does not divide the layer");
-  for (int rho = 0; rho < R; ++rho) {
-    const int nat = natural_of_packed(rho);
-    const int ab = nat / L.cout, o = nat % L.cout;
-    for (int c = 0; c < L.cin; ++c) {
-      const size_t idx = ring ? (((size_t)(rho / BR) * S + c / BKE) * BR + rho % BR) * BKE + c % BKE
-                              : (size_t)rho * L.cin + c;
-      put_elem(L.dt, buf, idx, W[(((size_t)c * L.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]);
+  std::vector<uint8_t> buf((size_t)R * L.cin * (L.x3 == 2 ? 6 : dtype_size(L.dt)));
+  if (L.x3 == 2) {   // the three-term plan: pre-split planes per (row tile, chunk), as pack3x3_split with one tap
+    const int BR = cfg_rows(L.cfg), NCH = L.cin / 32;
+    if (R % BR || L.cin % 32) return fail(UNET_EINVAL, "pre-split ConvTranspose tiling does not divide the layer");
+    for (int rho = 0; rho < R; ++rho) {
+      const int nat = natural_of_packed(rho), ab = nat / L.cout, o = nat % L.cout;
+      for (int ch = 0; ch < NCH; ++ch)
+        put_split_row(buf, ((size_t)(rho / BR) * NCH + ch) * 3 * BR * 64, BR, rho % BR, ch,
+                      [&](int c) { return W[(((size_t)c * L.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]; });
+    }
+  } else {
+    const bool ring = cfg_is_tring(L.cfg);
+    const int BR = cfg_rows(L.cfg), BKE = 64 / (int)dtype_size(L.dt), S = L.cin / BKE;
+    if (ring && (R % BR || L.cin % BKE)) return fail(UNET_EINVAL, "ring ConvTranspose tiling does not divide the layer");
+    for (int rho = 0; rho < R; ++rho) {
+      const int nat = natural_of_packed(rho);
+      const int ab = nat / L.cout, o = nat % L.cout;
+      for (int c = 0; c < L.cin; ++c) {
+        const size_t idx = ring ? (((size_t)(rho / BR) * S + c / BKE) * BR + rho % BR) * BKE + c % BKE
+                                : (size_t)rho * L.cin + c;
+        put_elem(L.dt, buf, idx, W[(((size_t)c * L.cout + o) * 2 + (ab >> 1)) * 2 + (ab & 1)]);
+      }
     }
   }
   std::vector<float> bias(R);
@@ -788,8 +812,8 @@ std::string layer_label(const unet_handle* h, const Layer& L, int epi, Split sp 
     std::snprintf(buf, sizeof buf, "conv3x3_ring_kernel<%s, 1, 4, %d, %d, %d, %d, %d, %s, %s, %d, %d>", tname(L.dt),
                   cfg_rows(cfg) / 16, ring_ns(cfg), epi, ring_tps(cfg), cfg == CFG_RING_FUSED_IN ? 1 : 0,
                   tname(L.dto), tname(epi == EPI_POOL ? L.dtq : L.dto), cfg_tile_h(cfg), cfg_tile_w(cfg));
-  } else if (L.x3 == 3) {
-    std::snprintf(buf, sizeof buf, "conv3x3_x3s_kernel<%d>", epi);
+  } else if (L.x3 == 3 || L.x3 == 4) {
+    std::snprintf(buf, sizeof buf, L.x3 == 3 ? "conv3x3_x3s_kernel<%d>" : "conv3x3_x3w_kernel<%d>", epi);
   } else {
     const int wpx = cfg == CFG_HALO_R64_W8 ? 8 : 4, tc = cfg == CFG_HALO_R128 ? 8 : 4,
               ns = L.x3 == 2 ? 2 : cfg == CFG_HALO_R128 ? 2 : 3;
@@ -819,8 +843,9 @@ void build_labels_at(const unet_handle* h, int N, int H, int W, std::string (&ou
     if (id >= 100) {   // a fused up1 launches nothing: empty label (tools: its time and work go to conv2.3)
       const int j = id - 100;
       out[i] = (j == 3 && h->fuse_up1) ? std::string()
-                                       : layer_label(h, h->U[j], EPI_UPSCATTER,
-                                                     layer_split(h, 17 + j, h->U[j], EPI_UPSCATTER, N, H >> kUpLevel[j], W >> kUpLevel[j]));
+                                       : layer_label(h, up_layer(h, j, N), EPI_UPSCATTER,
+                                                     layer_split(h, 17 + j, up_layer(h, j, N), EPI_UPSCATTER, N,
+                                                                 H >> kUpLevel[j], W >> kUpLevel[j]));
       continue;
     }
     int epi = id == C1B ? EPI_HEAD : (id == D1B || id == D2B || id == D3B || id == D4B) ? EPI_POOL : EPI_STORE;
@@ -979,10 +1004,17 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     const bool pool = i == D1B || i == D2B || i == D3B || i == D4B;
     if (cfg_is_halo(c) && (L.dto != L.dt || (pool && L.dtq != L.dt))) c = L.cout == 64 || pool ? CFG_RING_R64_T3 : CFG_RING_R128;
     if (c == CFG_RING_R128 && pool) c = CFG_RING_R64_T3;   // pooled 128-row 4-wave tiles spill: same family, 64 rows
-    if (h->f32x3 && f32) {   // the three-term plan: pre-split weights on 128-row split-once or 64-row tiles
-      const bool once = h->f32x3 == 2 && L.cout % 128 == 0 && i != C1B;
-      c = once ? CFG_HALO_R128 : CFG_HALO_R64_W4;
-      L.x3 = once ? 3 : 2;
+    if (h->f32x3 && f32) {   // the three-term plan: pre-split weights; split-once tiles (f32x3 = 2) of 128 rows
+                             // x 16x16 pixels where Cout >= 128 and Cin >= 128, 64 rows x 16x32 on conv1.3 (its
+                             // head epilogue on whole 32-pixel rows), split per tap on 64-row tiles elsewhere (a
+                             // one-block-per-CU tile exposes its prologue and epilogue: short-K layers lose)
+#ifndef UNET_X3_ONCE_MIN_CIN
+#define UNET_X3_ONCE_MIN_CIN 128
+#endif
+      const bool once = h->f32x3 == 2 && L.cout % 128 == 0 && L.cin >= UNET_X3_ONCE_MIN_CIN && i != C1B;
+      const bool wide = h->f32x3 == 2 && i == C1B;
+      c = once ? CFG_HALO_R128 : wide ? CFG_HALO_X3W : CFG_HALO_R64_W4;
+      L.x3 = once ? 3 : wide ? 4 : 2;
     }
     L.cfg = c;
   }
@@ -995,9 +1027,14 @@ int unet_create(const unet_config* cfg, unet_handle** out) {
     U.dt = level_dtype(cfg->dtype, kUpLevel[i]);
     U.dto = U.dtq = level_dtype(cfg->dtype, kUpLevel[i] - 1);
     U.cfg = (ucfgs[i] == CFG_HALO_R128 && U.dto != U.dt) ? (int)CFG_TRING_R256 : ucfgs[i];
-    if (h->f32x3 && f32) {   // both operands split on the fly (the fp32 ConvTranspose packing)
+    if (h->f32x3 && f32) {   // both operands split on the fly on 128-row tiles
       U.cfg = CFG_HALO_R128;
       U.x3 = 1;
+      if (h->f32x3 == 2) {   // + the small-batch variant: pre-split weights on 64-row tiles (two blocks per CU)
+        h->Us[i] = U;
+        h->Us[i].cfg = CFG_HALO_R64_W4;
+        h->Us[i].x3 = 2;
+      }
     }
   }
   {
@@ -1131,6 +1168,7 @@ int unet_load_weights(unet_handle* h, const unet_tensor_view* t, int n) {
     rc = check_f16_range(L.dt, std::vector<double>(W, W + (size_t)L.cin * L.cout * 4), std::vector<double>(B, B + L.cout),
                          kUpKey[i]);
     if (!rc) rc = packT(h, h->U[i], W, B);
+    if (!rc && h->Us[i].x3) rc = packT(h, h->Us[i], W, B);
     if (rc) return rc;
     if (i == 3 && h->fuse_up1) {   // conv2.3 + up1 in one launch
       rc = fold(sd, kLayerKey[C2B][0], kLayerKey[C2B][1], h->L[C2B].cin, h->L[C2B].cout, w, b);
@@ -1220,7 +1258,8 @@ int run_igemm(unet_handle* h, const Layer& L, int epi, const void* in, int N, in
   a.tiles_x = (W + cfg_tile_w(L.cfg) - 1) / cfg_tile_w(L.cfg);
   a.tiles_y = (H + cfg_tile_h(L.cfg) - 1) / cfg_tile_h(L.cfg);
   a.n_ct = L.ctot / cfg_rows(L.cfg);
-  const int id = (&L >= h->L && &L < h->L + 17) ? (int)(&L - h->L) : 17 + (int)(&L - h->U);
+  const int id = (&L >= h->L && &L < h->L + 17) ? (int)(&L - h->L)
+                 : (&L >= h->Us && &L < h->Us + 4) ? 17 + (int)(&L - h->Us) : 17 + (int)(&L - h->U);
   const Split sp = layer_split(h, id, L, epi, N, H, W);
   int cfg = L.cfg;
   if (sp.ks == 1 && sp.rows) {   // small-batch plan, unsplit: finer row tiles over the layer's packing
@@ -1322,20 +1361,20 @@ int forward_impl(unet_handle* h, const void* x, int x_layout, int x_dtype, void*
   RUN(h, h->L[BNA], EPI_STORE, buf(B.p4), N, H16, W16, 512, buf(B.tA), 1024, 0, nullptr, 0, s);
   RUN(h, h->L[BNB], EPI_STORE, buf(B.tA), N, H16, W16, 1024, buf(B.bnb), 1024, 0, nullptr, 0, s);
   // decoder: up_k writes the lower half of the concat buffer, conv_k reads all of it
-  RUN(h, h->U[0], EPI_UPSCATTER, buf(B.bnb), N, H16, W16, 1024, buf(B.cat4), 1024, 0, nullptr, 0, s);
+  RUN(h, up_layer(h, 0, N), EPI_UPSCATTER, buf(B.bnb), N, H16, W16, 1024, buf(B.cat4), 1024, 0, nullptr, 0, s);
   RUN(h, h->L[C4A], EPI_STORE, buf(B.cat4), N, H8, W8, 1024, buf(B.tA), 512, 0, nullptr, 0, s);
   RUN(h, h->L[C4B], EPI_STORE, buf(B.tA), N, H8, W8, 512, buf(B.tB), 512, 0, nullptr, 0, s);
-  RUN(h, h->U[1], EPI_UPSCATTER, buf(B.tB), N, H8, W8, 512, buf(B.cat3), 512, 0, nullptr, 0, s);
+  RUN(h, up_layer(h, 1, N), EPI_UPSCATTER, buf(B.tB), N, H8, W8, 512, buf(B.cat3), 512, 0, nullptr, 0, s);
   RUN(h, h->L[C3A], EPI_STORE, buf(B.cat3), N, H4, W4, 512, buf(B.tA), 256, 0, nullptr, 0, s);
   RUN(h, h->L[C3B], EPI_STORE, buf(B.tA), N, H4, W4, 256, buf(B.tB), 256, 0, nullptr, 0, s);
-  RUN(h, h->U[2], EPI_UPSCATTER, buf(B.tB), N, H4, W4, 256, buf(B.cat2), 256, 0, nullptr, 0, s);
+  RUN(h, up_layer(h, 2, N), EPI_UPSCATTER, buf(B.tB), N, H4, W4, 256, buf(B.cat2), 256, 0, nullptr, 0, s);
   RUN(h, h->L[C2A], EPI_STORE, buf(B.cat2), N, H2, W2, 256, buf(B.tA), 128, 0, nullptr, 0, s);
   if (h->fuse_up1) {   // conv2.3 + up1 in one launch (EPI_UPFUSE): up1's slot launches nothing
     RUN(h, h->L[C2B], EPI_UPFUSE, buf(B.tA), N, H2, W2, 128, nullptr, 0, 0, buf(B.cat1), 128, s);
     mark();
   } else {
     RUN(h, h->L[C2B], EPI_STORE, buf(B.tA), N, H2, W2, 128, buf(B.tB), 128, 0, nullptr, 0, s);
-    RUN(h, h->U[3], EPI_UPSCATTER, buf(B.tB), N, H2, W2, 128, buf(B.cat1), 128, 0, nullptr, 0, s);
+    RUN(h, up_layer(h, 3, N), EPI_UPSCATTER, buf(B.tB), N, H2, W2, 128, buf(B.cat1), 128, 0, nullptr, 0, s);
   }
   RUN(h, h->L[C1A], EPI_STORE, buf(B.cat1), N, H, W, 128, buf(B.tA), 64, 0, nullptr, 0, s);
   // conv1.net.3 + BN + ReLU + out_conv (1x1) + sigmoid/threshold, one launch

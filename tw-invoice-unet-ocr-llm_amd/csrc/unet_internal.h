@@ -68,7 +68,8 @@ struct IgemmArgs {
                 // bf16 terms (6 bf16 MFMAs per 32 K): 1 = both split on the fly (the ConvTranspose), 2 = weights
                 // pre-split by the packing, activations on the fly (3x3 layers, CFG_HALO_R64_W4), 3 = weights
                 // pre-split, activations split once per chunk into LDS planes (conv3x3_x3s_kernel,
-                // CFG_HALO_R128: the 3x3 layers with Cout >= 128)
+                // CFG_HALO_R128: the 3x3 layers with Cout >= 128), 4 = the same on 64 rows x 16x32 pixels
+                // from a register-prefetched halo (conv3x3_x3w_kernel, CFG_HALO_X3W: the 64-channel layers)
 };
 
 struct FirstConvArgs {
@@ -111,14 +112,17 @@ enum Cfg : int {
   // 16x16 tile's MFMAs per weight byte), one tap per step, 4 weight slots (64-row layers).
   // Rejected on A/B (3x the barriers of the T3 ring): built only in `make abl`
   CFG_RING_R64_W12 = 12,
-  CFG_COUNT = 13
+  // the three-term fp32 plan's 64-channel layers: 64 rows x 16x32 pixels, 8 waves, activations split once
+  // per chunk from a register-prefetched halo (conv3x3_x3w_kernel; set by the plan only, not an override)
+  CFG_HALO_X3W = 13,
+  CFG_COUNT = 14
 };
 int cfg_rows(int cfg);
 bool cfg_is_halo(int cfg);
 bool cfg_is_ring(int cfg);   // 64-byte-row ring kernel: step-major packed weights
 int ring_ns(int cfg);       // ring kernel: weight-ring slots
 int ring_tps(int cfg);      // ring kernel: taps per step
-int cfg_tile_w(int cfg);    // pixel-tile width (16, or 32 for the 8-wave ring and CFG_RING_R64_W12)
+int cfg_tile_w(int cfg);    // pixel-tile width (16, or 32 for the 8-wave ring, CFG_RING_R64_W12 and CFG_HALO_X3W)
 int cfg_tile_h(int cfg);    // pixel-tile height (16, or 12 for CFG_RING_R64_W12)
 bool cfg_is_ring8(int cfg); // the 8-wave ring kernel (conv3x3_ring8_kernel)
 bool cfg_fused_in(int cfg); // down1.0 fused into down1.3 (the network input feeds the kernel)

@@ -40,7 +40,9 @@ int cfg_rows(int cfg) {
     default: return 64;
   }
 }
-bool cfg_is_halo(int cfg) { return cfg == CFG_HALO_R64_W4 || cfg == CFG_HALO_R64_W8 || cfg == CFG_HALO_R128; }
+bool cfg_is_halo(int cfg) {
+  return cfg == CFG_HALO_R64_W4 || cfg == CFG_HALO_R64_W8 || cfg == CFG_HALO_R128 || cfg == CFG_HALO_X3W;
+}
 bool cfg_is_ring(int cfg) {
   cfg %= 16;
   return cfg == CFG_RING_R128 || cfg == CFG_RING_R64_T3 || cfg == CFG_RING_FUSED_IN || cfg == CFG_RING8_R128 ||
@@ -50,7 +52,9 @@ bool cfg_is_ring8(int cfg) {
   cfg %= 16;
   return cfg == CFG_RING8_R128 || cfg == CFG_RING8_R64_T9 || cfg == CFG_RING8_R64_WS || cfg == CFG_RING8_FUSED_IN;
 }
-int cfg_tile_w(int cfg) { return (cfg_is_ring8(cfg) || cfg % 16 == CFG_RING_R64_W12) ? 32 : 16; }
+int cfg_tile_w(int cfg) {
+  return (cfg_is_ring8(cfg) || cfg % 16 == CFG_RING_R64_W12 || cfg == CFG_HALO_X3W) ? 32 : 16;
+}
 int cfg_tile_h(int cfg) { return cfg % 16 == CFG_RING_R64_W12 ? 12 : 16; }
 bool cfg_fused_in(int cfg) { return cfg % 16 == CFG_RING_FUSED_IN || cfg % 16 == CFG_RING8_FUSED_IN; }
 int ring_ns(int cfg) { return cfg % 16 == CFG_RING_R64_W12 ? 4 : (cfg % 16 == CFG_RING8_R64_T9 ? 2 : 3); }
@@ -1241,6 +1245,176 @@ __global__ __launch_bounds__(512, 1) void conv3x3_x3s_kernel(const IgemmArgs a) 
   else
     conv_epilogue<float, float, TP, EPI>(a, acc, n, ty * 16, tx * 16, wp * TP, row0, bias_s + wr * 16 * TC, nullptr,
                                          nullptr);
+}
+
+// The 64-channel layers of the three-term plan (down1.3 + pool, conv1.0, conv1.3 + head; IgemmArgs::x3 = 4):
+// the split-once scheme above on 64 rows x 16x32 pixels, 8 waves of one row pair x 32 columns (the 16-bit
+// ring's tile and head epilogue), one block per CU.  The 18x34 halo's three planes take 115 KB, which
+// leaves no room for an fp32 staging copy: each thread prefetches its five (pixel, piece) units of the next
+// chunk into registers (40 VGPRs, issued behind the step's weights at the chunk's first tap) and splits them
+// into the planes at the chunk's end.  Planes as conv3x3_x3s_kernel (pixel
+// r = hy * 34 + hx, 34 = 2 mod 4 like 18: the same bank argument, tests/test_lds_layout_cpu.py).
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void conv3x3_x3w_kernel(const IgemmArgs a) {
+  constexpr int NW = 8, TC = 4, TP = 4, BR = 64, TW = 32, HWX = TW + 2, NPIX = 18 * HWX, NTAP = 9;
+  constexpr int NU = NPIX * 4;                          // (pixel, piece) units of a chunk
+  constexpr int UPT = (NU + 64 * NW - 1) / (64 * NW);   // per thread (past NU: loads of the zero page)
+  constexpr int PLANE = NPIX * 64;
+  constexpr int WSLOT = 3 * BR * 64;                    // 12 DMA pieces: waves 0..3 issue two
+  constexpr int WOFF = 3 * PLANE;
+  constexpr int PARAM_OFF = WOFF + 2 * WSLOT;
+  constexpr int LDS_BYTES = PARAM_OFF + (BR + kMaxClasses * 64 + kMaxClasses) * 4;
+  static_assert(LDS_BYTES <= 160 * 1024 && WSLOT == 12 * 1024, "one 8-wave block per CU");
+  static_assert(PLANE % 256 == 0 && WOFF % 256 == 0, "bank-aligned regions");
+  static_assert(EPI == EPI_STORE || EPI == EPI_POOL || EPI == EPI_HEAD || EPI == EPI_PARTIAL, "x3w epilogues");
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  float* bias_s = reinterpret_cast<float*>(lds + PARAM_OFF);
+  float* headw_s = bias_s + BR;
+  float* headb_s = headw_s + kMaxClasses * 64;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  int bid;
+  {  // XCD-contiguous remap (as conv3x3_halo_kernel)
+    const int nb = gridDim.x, qq = nb >> 3, rr = nb & 7;
+    const int b = blockIdx.x, x = b & 7, k = b >> 3;
+    bid = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + k;
+  }
+  constexpr bool PART = EPI == EPI_PARTIAL;
+  const int KS = PART ? a.ksplit : 1;
+  const int ct = bid % a.n_ct;
+  int mt = bid / a.n_ct;
+  const int kslice = PART ? mt % KS : 0;
+  if (PART) mt /= KS;
+  const int tx = mt % a.tiles_x;
+  mt /= a.tiles_x;
+  const int ty = mt % a.tiles_y;
+  const int n = mt / a.tiles_y;
+  if (n >= a.N) return;
+
+  const int H = a.H, W = a.W;
+  const int nch = a.Cin / 32 / KS;
+  const int c_lo = kslice * nch;
+  const int S = NTAP * nch;
+  const float* in = reinterpret_cast<const float*>(a.in);
+  const float* zero = reinterpret_cast<const float*>(a.zero);
+  const long long pix0 = (long long)(n * H + ty * 16) * W + tx * TW;
+
+  frag_t hv[UPT][2];   // the next chunk's units: fp32 K values 4q..4q+3 and 16+4q..16+4q+3 of one pixel
+  auto load_halo = [&](int c) {
+    const long long c0 = (long long)c * 32;
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int u = tid + k * 64 * NW;
+      const int r = u >> 2, pq = u & 3;
+      const int hy = r / HWX, hx = r - hy * HWX;
+      const int iy = ty * 16 + hy - 1, ix = tx * TW + hx - 1;
+      const bool ok = u < NU && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const float* src = ok ? in + (pix0 + (long long)(hy - 1) * W + (hx - 1)) * a.ldi + c0 : zero;
+      hv[k][0] = *reinterpret_cast<const frag_t*>(src + 4 * pq);
+      hv[k][1] = *reinterpret_cast<const frag_t*>(src + 16 + 4 * pq);
+    }
+  };
+  auto split_halo = [&]() {
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int u = tid + k * 64 * NW;
+      if (u < NU) {
+        const int r = u >> 2, pq = u & 3, hy = r / HWX;
+        frag_t h, m, l;
+        split3_bf16(hv[k][0], hv[k][1], h, m, l);
+        char* dp = lds + r * 64 + ((pq ^ ((hy & 1) << 1)) << 4);
+        *reinterpret_cast<frag_t*>(dp) = h;
+        *reinterpret_cast<frag_t*>(dp + PLANE) = m;
+        *reinterpret_cast<frag_t*>(dp + 2 * PLANE) = l;
+      }
+    }
+  };
+  auto issue_w = [&](int g) {   // step g's pre-split weights [3][64][64 B] (unet_capi.cpp pack3x3_split)
+    const long long step = (long long)ct * (NTAP * (a.Cin / 32)) + (long long)c_lo * NTAP + g;
+    const char* src = reinterpret_cast<const char*>(a.wgt) + step * WSLOT + lane * 16;
+    char* dst = lds + WOFF + (g & 1) * WSLOT;
+    glds16(src + wave * 1024, dst + wave * 1024);
+    if (wave < 4) glds16(src + (wave + 8) * 1024, dst + (wave + 8) * 1024);
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int t = 0; t < TC; ++t)
+#pragma unroll
+    for (int p = 0; p < TP; ++p) acc[t][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int col = lane & 15, q = lane >> 4;
+  int prow[TP];
+#pragma unroll
+  for (int p = 0; p < TP; ++p) {
+    int py, px;
+    pix_of_w<TW>((wave * TP + p) * 16 + col, py, px);
+    prow[p] = py * HWX + px;
+  }
+  const int ylo = (col >> 3) & 1;   // hy & 1 of this lane's pixels at dy = 0
+  const char* Wl = lds + WOFF + col * 64 + ((q ^ ((col >> 1) & 3)) << 4);
+
+  load_halo(c_lo);
+  issue_w(0);
+  for (int i = tid; i < BR; i += 64 * NW) bias_s[i] = a.bias[ct * BR + i];
+  if (EPI == EPI_HEAD) {
+    for (int i = tid; i < a.ncls * 64; i += 64 * NW) headw_s[i] = a.head_w[i];
+    if (tid < a.ncls) headb_s[tid] = a.head_b[tid];
+  }
+  split_halo();
+  wait_vm_barrier<0>();
+
+  // The next chunk's halo loads go out at the chunk's first tap, behind W(g + 1), and retire with it at
+  // that step's vmcnt(0): a step of MFMAs covers both.  (Left in flight for a second step, the compiler's
+  // own wait tracking -- blind to the asm weight DMAs, path-insensitive over the loop -- put a vmcnt(0)
+  // in front of the next chunk's loads that also waited for the weights.)
+  int c = 0, tap = 0;
+  for (int g = 0; g < S; ++g) {
+    if (g + 1 < S) issue_w(g + 1);
+    if (tap == 0 && c + 1 < nch) load_halo(c_lo + c + 1);
+    {
+      const int dy = tap / 3, dx = tap - dy * 3;
+      const char* Wp = Wl + (g & 1) * WSLOT;
+      frag_t ah[TC], am[TC], al[TC];
+#pragma unroll
+      for (int t = 0; t < TC; ++t) {
+        ah[t] = *reinterpret_cast<const frag_t*>(Wp + t * 16 * 64);
+        am[t] = *reinterpret_cast<const frag_t*>(Wp + BR * 64 + t * 16 * 64);
+        al[t] = *reinterpret_cast<const frag_t*>(Wp + 2 * BR * 64 + t * 16 * 64);
+      }
+      const char* Bl = lds + (dy * HWX + dx) * 64 + ((q ^ (((ylo ^ dy) & 1) << 1)) << 4);
+#pragma unroll
+      for (int p = 0; p < TP; ++p) {
+        const char* bp = Bl + prow[p] * 64;
+        const frag_t bh = *reinterpret_cast<const frag_t*>(bp);
+        const frag_t bm = *reinterpret_cast<const frag_t*>(bp + PLANE);
+        const frag_t bl = *reinterpret_cast<const frag_t*>(bp + 2 * PLANE);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], am[t], bm);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], al[t], bh);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], ah[t], bl);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], am[t], bh);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], ah[t], bm);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], ah[t], bh);
+      }
+    }
+    wait_vm_barrier<0>();
+    if (tap == NTAP - 1 && c + 1 < nch) {   // every wave is past the chunk's last tap: refill the planes
+      split_halo();
+      wait_vm_barrier<0>();
+    }
+    if (++tap == NTAP) { tap = 0; ++c; }
+  }
+  if constexpr (PART)
+    partial_store<TP, TW>(a, acc, n, ty * 16, tx * TW, wave * TP, ct * BR, kslice);
+  else
+    conv_epilogue<float, float, TP, EPI, TW>(a, acc, n, ty * 16, tx * TW, wave * TP, ct * BR, bias_s, headw_s, headb_s);
 }
 
 
@@ -2845,7 +3019,7 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
         return hipGetLastError();
       }
     }
-    if constexpr (sizeof(T) == 4 && WPX == 4 && TCW == 4 && KT == 3) {
+    if constexpr (sizeof(T) == 4 && WPX == 4 && TCW == 4) {   // (KT = 1: the ConvTranspose, one tap)
       if (a.x3 == 2) {
         hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, 2, KT, EPI, 2>), dim3((unsigned)nb),
                            dim3(64 * WR * WPX), 0, s, a);
@@ -2863,6 +3037,19 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   }
   hipLaunchKernelGGL((conv3x3_halo_kernel<T, WR, WPX, TCW, NS, KT, EPI>), dim3((unsigned)nb), dim3(64 * WR * WPX), 0,
                      s, a);
+  return hipGetLastError();
+}
+
+// the three-term plan's 64-channel layers (x3 = 4): 64 rows x 16x32 pixels per block
+template <int EPI>
+static hipError_t launch_x3w(const IgemmArgs& a, hipStream_t s) {
+  if (a.x3 != 4 || a.tiles_y != (a.H + 15) / 16 || a.tiles_x != (a.W + 31) / 32) return hipErrorInvalidValue;
+  if (a.Cin % 32 || a.Ctot % 64 || a.n_ct != a.Ctot / 64 || (EPI == EPI_HEAD && a.n_ct != 1)) return hipErrorInvalidValue;
+  const int KS = EPI == EPI_PARTIAL ? a.ksplit : 1;
+  if (KS < 1 || a.Cin % (32 * KS) || (EPI == EPI_PARTIAL && !a.part)) return hipErrorInvalidValue;
+  const long long nb = (long long)a.n_ct * KS * a.N * a.tiles_y * a.tiles_x;
+  if (nb <= 0 || nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((conv3x3_x3w_kernel<EPI>), dim3((unsigned)nb), dim3(512), 0, s, a);
   return hipGetLastError();
 }
 
@@ -2927,6 +3114,7 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
         case CFG_HALO_R64_W4: if constexpr (sizeof(T) == 4) return launch_halo<T, 1, 4, 4, 3, EPI, 3>(a, s); break;
         case CFG_HALO_R64_W8: if constexpr (sizeof(T) == 4) return launch_halo<T, 1, 8, 4, 3, EPI, 3>(a, s); break;
         case CFG_HALO_R128: if constexpr (sizeof(T) == 4) return launch_halo<T, 1, 4, 8, 2, EPI, 3>(a, s); break;
+        case CFG_HALO_X3W: if constexpr (sizeof(T) == 4) return launch_x3w<EPI>(a, s); break;
         case CFG_RING8_R128:   // 128-row tiles, or 64-row tiles over the 128-row packing (a.src_br)
           if constexpr (sizeof(T) == 2) {
             if (a.src_br == 128) return launch_ring8<T, 4, 3, EPI, 3, 0, T, T>(a, s);
@@ -2967,6 +3155,10 @@ static hipError_t launch_3x3(int cfg, const IgemmArgs& a, hipStream_t s) {
     case CFG_HALO_R64_W4: if constexpr (same) return launch_halo<T, 1, 4, 4, 3, EPI, 3>(a, s); break;
     case CFG_HALO_R64_W8: if constexpr (same) return launch_halo<T, 1, 8, 4, 3, EPI, 3>(a, s); break;
     case CFG_HALO_R128: if constexpr (same && EPI != EPI_HEAD) return launch_halo<T, 1, 4, 8, 2, EPI, 3>(a, s); break;
+    case CFG_HALO_X3W:
+      if constexpr (same && sizeof(T) == 4 && (EPI == EPI_STORE || EPI == EPI_POOL || EPI == EPI_HEAD))
+        return launch_x3w<EPI>(a, s);
+      break;
     // (pooled 128-row 4-wave tiles spill two VGPRs: not built; unet_capi runs those layers on 64-row tiles)
     case CFG_RING_R128: if constexpr (EPI != EPI_HEAD && EPI != EPI_POOL) return launch_ring<T, 1, 4, 8, 3, EPI, 1, 0, TO, TQ>(a, s); break;
     case CFG_RING_R64_T3: return launch_ring<T, 1, 4, 4, 3, EPI, 3, 0, TO, TQ>(a, s);
@@ -3001,11 +3193,17 @@ template <typename T, typename TO, int EPI = EPI_UPSCATTER>
 static hipError_t launch_up(int cfg, const IgemmArgs& a, hipStream_t s) {
   if constexpr (EPI == EPI_PARTIAL) {   // split-K slices of the LDS-halo ConvTranspose (the fp32 path)
     if (cfg == CFG_HALO_R128) return launch_halo<T, 1, 4, 8, 2, EPI_PARTIAL, 1>(a, s);
+    if constexpr (sizeof(T) == 4)
+      if (cfg == CFG_HALO_R64_W4 && a.x3 == 2) return launch_halo<T, 1, 4, 4, 2, EPI_PARTIAL, 1>(a, s);
     return hipErrorInvalidValue;
   }
   switch (cfg) {
     case CFG_HALO_R128:
       if constexpr (std::is_same<T, TO>::value) return launch_halo<T, 1, 4, 8, 2, EPI_UPSCATTER, 1>(a, s);
+      break;
+    case CFG_HALO_R64_W4:   // the three-term plan's pre-split 64-row tiles only
+      if constexpr (std::is_same<T, TO>::value && sizeof(T) == 4)
+        if (a.x3 == 2) return launch_halo<T, 1, 4, 4, 2, EPI_UPSCATTER, 1>(a, s);
       break;
     case CFG_TRING_R128: return launch_tring<T, 8, 3, 1, TO>(a, s);
     case CFG_TRING_R256: return launch_tring<T, 8, 4, 2, TO>(a, s);
