@@ -1202,6 +1202,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_x3s_kernel(const IgemmArgs a) 
     {
       const int dy = tap / 3, dx = tap - dy * 3;
       const char* Wp = Wl + (g & 1) * WSLOT;
+      const char* Bl = lds + SPL + (dy * HWD + dx) * 64 + ((q ^ (((ylo ^ dy) & 1) << 1)) << 4);
       frag_t ah[TC], am[TC], al[TC];
 #pragma unroll
       for (int t = 0; t < TC; ++t) {
@@ -1209,7 +1210,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_x3s_kernel(const IgemmArgs a) 
         am[t] = *reinterpret_cast<const frag_t*>(Wp + BR * 64 + t * 16 * 64);
         al[t] = *reinterpret_cast<const frag_t*>(Wp + 2 * BR * 64 + t * 16 * 64);
       }
-      const char* Bl = lds + SPL + (dy * HWD + dx) * 64 + ((q ^ (((ylo ^ dy) & 1) << 1)) << 4);
 #pragma unroll
       for (int p = 0; p < TP; ++p) {
         const char* bp = Bl + prow[p] * 64;
@@ -2892,12 +2892,16 @@ __global__ __launch_bounds__(256) void first_conv_kernel(const FirstConvArgs a) 
   constexpr int KW = 9 * C;
   __shared__ float ws[64 * KW];
   __shared__ float bs[64];
+  __shared__ float xs_out[sizeof(T) == 4 ? 256 * 33 : 1];   // fp32: one 32-channel half of the block's outputs
   for (int i = threadIdx.x; i < 64 * KW; i += 256) ws[i] = a.w[i];
   if (threadIdx.x < 64) bs[threadIdx.x] = a.b[threadIdx.x];
   __syncthreads();
   const int total = a.N * a.H * a.W;   // <= 2^30 (unet_capi's shape check): 32-bit index math
-  const int pix = blockIdx.x * 256 + threadIdx.x;
-  if (pix >= total) return;
+  int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= total) {
+    if constexpr (sizeof(T) != 4) return;
+    pix = total - 1;   // (fp32: every thread reaches the block's barriers; its stores are masked)
+  }
   const int x = pix % a.W;
   const int t = pix / a.W;
   const int y = t % a.H;
@@ -2913,19 +2917,50 @@ __global__ __launch_bounds__(256) void first_conv_kernel(const FirstConvArgs a) 
         const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
         xin[(c * 3 + ky) * 3 + kx] = ok ? a.x[(((long long)n * C + c) * a.H + iy) * a.W + ix] : 0.f;
       }
-  T* dst = reinterpret_cast<T*>(a.out) + (long long)pix * 64;
+  if constexpr (sizeof(T) == 4) {
+    // fp32 out: 256 B per pixel.  A lane's own 64-byte stores would leave each store instruction scattered
+    // over 64 pixels (16 KB); instead each 32-channel half goes through LDS and leaves as whole 128-byte
+    // pixel runs, 8 lanes per pixel (round 6: the per-lane form moved 2.1 GB at ~2.6 TB/s)
+    float* tile = xs_out;
+    const int p0 = blockIdx.x * 256;
+    const int npx = min(256, total - p0);
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    float v[16];
+    for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int co = g * 16 + e;
-      float s = 0.f;
+      for (int e = 0; e < 32; ++e) {
+        const int co = h * 32 + e;
+        float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < KW; ++k) s = fmaf(ws[co * KW + k], xin[k], s);
-      v[e] = relu_nan(s + bs[co]);
+        for (int k = 0; k < KW; ++k) s = fmaf(ws[co * KW + k], xin[k], s);
+        tile[threadIdx.x * 33 + e] = relu_nan(s + bs[co]);
+      }
+      __syncthreads();
+      float* out = reinterpret_cast<float*>(a.out) + (long long)p0 * 64 + h * 32;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int u = it * 256 + threadIdx.x, px = u >> 3, c4 = (u & 7) * 4;
+        if (px < npx) {
+          const float* sp = tile + px * 33 + c4;
+          *reinterpret_cast<f32x4*>(out + (long long)px * 64 + c4) = f32x4{sp[0], sp[1], sp[2], sp[3]};
+        }
+      }
+      __syncthreads();
     }
-    store16<T>(dst + g * 16, v);
+  } else {
+    T* dst = reinterpret_cast<T*>(a.out) + (long long)pix * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = g * 16 + e;
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) s = fmaf(ws[co * KW + k], xin[k], s);
+        v[e] = relu_nan(s + bs[co]);
+      }
+      store16<T>(dst + g * 16, v);
+    }
   }
 }
 
