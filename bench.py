@@ -651,6 +651,26 @@ def gpu_latency(args, runner, dev):
                 inf.run_unet(pil, ck, compute_dtype=dtype)
                 lat.append(time.perf_counter() - t0)
             out["run_unet_ms"] = round(1e3 * float(np.median(lat)), 3)
+            # photos of several sizes: six geometries in rotation, each graph cached after its
+            # first call; then more geometries than the photo-graph LRU holds, so every call captures anew
+            varied = [pil.resize(sz) for sz in ((600, 400), (640, 480), (800, 600), (500, 700), (1024, 768), (720, 540))]
+            for p in varied:
+                inf.run_unet(p, ck, compute_dtype=dtype)
+            lat = []
+            for _ in range(3):
+                for p in varied:
+                    t0 = time.perf_counter()
+                    inf.run_unet(p, ck, compute_dtype=dtype)
+                    lat.append(time.perf_counter() - t0)
+            out["run_unet_6_geometries_ms"] = round(1e3 * float(np.median(lat)), 3)
+            many = [pil.resize((400 + 16 * i, 300 + 12 * i)) for i in range(inf._Staging.MAX_GRAPHS + 4)]
+            lat = []
+            for _ in range(2):
+                for p in many:
+                    t0 = time.perf_counter()
+                    inf.run_unet(p, ck, compute_dtype=dtype)
+                    lat.append(time.perf_counter() - t0)
+            out["run_unet_lru_miss_ms"] = round(1e3 * float(np.median(lat)), 3)
             model = inf._cached_model(ck, dtype)
             h = model.native_handle(dev)
             x1 = torch.from_numpy(gen_pages(3, 1, 512, 3)).to(dev)
