@@ -750,7 +750,7 @@ struct HaloGeom {
   static constexpr int NPIX = HWD * HWD;
   static constexpr int NTAP = KT * KT;
   static constexpr int HI = (NPIX + 8 * NW - 1) / (8 * NW);   // halo DMA instructions per wave (at most)
-  // X3 = 2: a step's weights as three bf16 planes (hi, mid, lo) of BR rows x 64 B (unet_capi.cpp pack3x3_host);
+  // X3 = 2: a step's weights as three bf16 planes (hi, mid, lo) of BR rows x 64 B (unet_capi.cpp pack3x3_split);
   // the halo's 1 KB DMA pieces are dealt over the waves round-robin, only as many as the halo needs (NI),
   // so that three weight slots fit beside it at two blocks per CU
   static constexpr int WSLOT = X3 == 2 ? 3 * BR * 64 : BR * 128;
@@ -764,9 +764,9 @@ struct HaloGeom {
 
 // X3 (fp32 only): the fp32 operands as three bf16 terms (split3_bf16), 6 bf16 MFMAs per 32-K block instead of
 // 8 exact-fp32 ones, same epilogues.  X3 = 1: both operands split on the fly (same LDS images and weight
-// packing as the fp32 kernel; the ConvTranspose).  X3 = 2: the weights come pre-split from the packing as
-// three bf16 planes per step (no VALU for A, which the block's waves share), the activations are split on
-// the fly per fragment (the 3x3 layers).
+// packing as the fp32 kernel; the ConvTranspose at larger batches).  X3 = 2: the weights come pre-split from
+// the packing as three bf16 planes per step (no VALU for A, which the block's waves share), the activations
+// are split on the fly per fragment (the short-K 3x3 layers, the batch-1 ConvTranspose).
 template <typename T, int WR, int WPX, int TCW, int NS, int KT, int EPI, int X3 = 0>
 __global__ __launch_bounds__(64 * WR * WPX, 2 * WR * WPX / 4) void conv3x3_halo_kernel(const IgemmArgs a) {
   using G = HaloGeom<T, WR, WPX, TCW, NS, KT, X3>;
@@ -1193,12 +1193,28 @@ __global__ __launch_bounds__(512, 1) void conv3x3_x3s_kernel(const IgemmArgs a) 
   split_halo();
   wait_vm_barrier<0>();
 
-  int c = 0, tap = 0;
-  for (int g = 0; g < S; ++g) {
+  // one K step (chunk c, tap); LAST (the chunk's last tap, peeled so that it is its own code): the next
+  // chunk's staged halo (landed at tap 1's wait) is split into registers between this tap's MFMAs, and
+  // after the barrier only the plane stores remain exposed
+  constexpr int SR = (NPIX * 4 + 64 * NW - 1) / (64 * NW);   // split units per thread
+  auto step = [&](int c, int tap, auto last_tag) {
+    constexpr bool LAST = decltype(last_tag)::value;
+    const int g = c * NTAP + tap;
     if (g + 1 < S) issue_w(g + 1);
     // the next chunk's halo into the (free) staging buffer, behind W(g + 1): in flight for two steps
-    const bool hnext = tap == 0 && c + 1 < nch;
+    const bool hnext = !LAST && tap == 0 && c + 1 < nch;
     if (hnext) issue_halo(c_lo + c + 1);
+    frag_t sh[SR], sm[SR], sl[SR];
+    if constexpr (LAST) {
+#pragma unroll
+      for (int k = 0; k < SR; ++k) {   // (past the last unit: a valid row, split and dropped)
+        const int u = min(tid + k * 64 * NW, NPIX * 4 - 1);
+        const int r = u >> 2, pq = u & 3, hx7 = (r - (r / HWD) * HWD) & 7;
+        const char* sp = lds + r * 128;
+        split3_bf16(*reinterpret_cast<const frag_t*>(sp + ((pq ^ hx7) << 4)),
+                    *reinterpret_cast<const frag_t*>(sp + (((4 + pq) ^ hx7) << 4)), sh[k], sm[k], sl[k]);
+      }
+    }
     {
       const int dy = tap / 3, dx = tap - dy * 3;
       const char* Wp = Wl + (g & 1) * WSLOT;
@@ -1231,13 +1247,32 @@ __global__ __launch_bounds__(512, 1) void conv3x3_x3s_kernel(const IgemmArgs a) 
         for (int t = 0; t < TC; ++t) mfma_bf16(acc[t][p], ah[t], bh);
       }
     }
+    if constexpr (LAST) {   // the split is done before the barrier (else the compiler sinks it into the stores)
+#pragma unroll
+      for (int k = 0; k < SR; ++k) asm volatile("" ::"v"(sh[k]), "v"(sm[k]), "v"(sl[k]));
+    }
     // W(g + 1) landed (and the halo, one step later); the barrier's lgkmcnt(0) retires this step's reads
     if (hnext) wait_vm_barrier<HJ>(); else wait_vm_barrier<0>();
-    if (tap == NTAP - 1 && c + 1 < nch) {   // every wave is past the chunk's last tap: refill the planes
-      split_halo();
-      wait_vm_barrier<0>();
+    if constexpr (LAST) {
+      if (c + 1 < nch) {   // every wave is past the chunk's last tap: the planes take the next chunk
+#pragma unroll
+        for (int k = 0; k < SR; ++k) {
+          const int u = tid + k * 64 * NW;
+          if (u < NPIX * 4) {
+            const int r = u >> 2, pq = u & 3, hy = r / HWD;
+            char* dp = lds + SPL + r * 64 + ((pq ^ ((hy & 1) << 1)) << 4);
+            *reinterpret_cast<frag_t*>(dp) = sh[k];
+            *reinterpret_cast<frag_t*>(dp + PLANE) = sm[k];
+            *reinterpret_cast<frag_t*>(dp + 2 * PLANE) = sl[k];
+          }
+        }
+        wait_vm_barrier<0>();
+      }
     }
-    if (++tap == NTAP) { tap = 0; ++c; }
+  };
+  for (int c = 0; c < nch; ++c) {
+    for (int tap = 0; tap < NTAP - 1; ++tap) step(c, tap, std::false_type{});
+    step(c, NTAP - 1, std::true_type{});
   }
   const int row0 = ct * BR + wr * 16 * TC;
   if constexpr (PART)
@@ -3043,10 +3078,11 @@ static hipError_t launch_halo(const IgemmArgs& a, hipStream_t s) {
   // one block per (row tile, K slice, pixel tile)
   const long long nb = (long long)a.n_ct * KS * a.N * a.tiles_y * a.tiles_x;
   if (nb <= 0 || nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-  if (a.x3) {   // fp32 operands as three bf16 terms (split3_bf16): the 3x3 layers on 64-row 4-wave tiles with
-                // pre-split weights (two weight slots: a third beside the exactly sized halo fits, 78 KB, but
-                // measured 2 % slower), the
-                // ConvTranspose with both operands split on the fly
+  if (a.x3) {   // fp32 operands as three bf16 terms (split3_bf16): x3 = 3, the split-once 128-row tiles
+                // (conv3x3_x3s_kernel); x3 = 2, pre-split weights on 64-row 4-wave tiles, the activations split
+                // per tap (the short-K 3x3 layers; the batch-1 ConvTranspose, KT = 1) -- two weight slots: a
+                // third fits beside the exactly sized halo, 78 KB, but measured 2 % slower; x3 = 1, both
+                // operands split on the fly (the ConvTranspose at larger batches)
     if constexpr (sizeof(T) == 4 && WPX == 4 && TCW == 8 && KT == 3 &&
                   (EPI == EPI_STORE || EPI == EPI_POOL || EPI == EPI_PARTIAL)) {
       if (a.x3 == 3) {   // 128-row tiles, the activations split once per chunk (conv3x3_x3s_kernel)
