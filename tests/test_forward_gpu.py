@@ -1203,6 +1203,30 @@ def test_launch_labels_at_name_the_small_batch_kernels():
     m.close()
 
 
+def test_fp32_plan_kernels_per_layer():
+    """The three-term fp32 plan's kernel per launch: the VALU first conv; split-per-tap 64-row
+    tiles on the short-K layers (down1.3, down2.0, conv1.0); split-once 128-row tiles on the long-K layers;
+    the 16x32 split-once tile with the head on conv1.3; the ConvTranspose on 128-row tiles splitting both
+    operands at large batch and on pre-split 64-row tiles at batch 1."""
+    sd = syn.make_state_dict(0, 3, 3, "pretrained")
+    m = make_model(sd, 3, "fp32")
+    h = m.native_handle(torch.device(DEV))
+    big = h.launch_labels()
+    assert big[0] == "first_conv_kernel<float, 3>", big[0]
+    for i, epi in ((1, 1), (2, 0), (20, 0)):    # down1.3 (+ pool), down2.0, conv1.0
+        assert big[i] == f"conv3x3_halo_kernel<float, 1, 4, 4, 2, 3, {epi}, 2>", (i, big[i])
+    assert big[3] == "conv3x3_x3s_kernel<1>" and big[9] == "conv3x3_x3s_kernel<0>", (big[3], big[9])
+    assert big[21] == "conv3x3_x3w_kernel<2>", big[21]
+    for i in (10, 13, 16, 19):                   # up4 .. up1
+        assert big[i] == "conv3x3_halo_kernel<float, 1, 4, 8, 2, 1, 3, 1>", (i, big[i])
+    small = h.launch_labels_at(1, 512, 512)
+    for i in (10, 13, 16, 19):
+        assert small[i].startswith("conv3x3_halo_kernel<float, 1, 4, 4, 2, 1, ") and small[i].count(", 2>") >= 1, \
+            (i, small[i])
+    assert small[21] == big[21]
+    m.close()
+
+
 def _pool2(a):
     n, c, h, w = a.shape
     return a.reshape(n, c, h // 2, 2, w // 2, 2).max(axis=(3, 5))
