@@ -393,7 +393,12 @@ def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
     marks = iter(ev[1:]) if ev else iter(())
     ag_marks = iter(ag) if ag else iter(())
 
+    first = [bool(ev)]
+
     def timed_step():
+        if first[0]:   # step 0's start mark inside the timed region (after timed_steps' barrier + sync),
+            first[0] = False   # so a rank's compute time never includes the wait at that barrier
+            ev[0].record()
         pair = next(ag_marks, None)
         if pair is None:
             leg["step"]()
@@ -402,9 +407,6 @@ def time_leg(leg, steps, warmup, sync, dev, per_step_events=False):
         e = next(marks, None)
         if e is not None:
             e.record()
-    if ev:
-        sync()
-        ev[0].record()
     try:
         elapsed, host = udist.timed_steps(timed_step, steps, 0, sync=sync, device=dev, collective=collective)
     finally:
